@@ -1,0 +1,138 @@
+/*
+ * nwcrypto — MI355X-native Ed25519 verification and SHA-512 digesting for Narwhal/Bullshark.
+ *
+ * C ABI drop-in boundary for the reference ``crypto`` crate's hot path.
+ * Every entry point names the reference interface it replaces.  All buffers are caller-owned;
+ * calls are synchronous unless the name ends in ``_dev`` (those enqueue on a caller stream and
+ * take device pointers).  A context is safe to share between threads (calls serialize on it).
+ * There is no CPU fallback: with no usable GPU every call returns NW_ERR_DEVICE.
+ *
+ * Verdict semantics are those of ed25519-dalek 1.0.1 (default features + "batch"):
+ *   strict  = crypto::Signature::verify      (crypto/src/lib.rs:200-204) -> verify_strict
+ *   batch   = crypto::Signature::verify_batch (crypto/src/lib.rs:206-219) -> dalek::verify_batch,
+ *             with the random 128-bit coefficients drawn from a seeded ChaCha20 stream
+ *             (NW-Z v1, see nw_chacha.h) instead of thread_rng.
+ */
+#ifndef NWCRYPTO_H
+#define NWCRYPTO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Status codes.  NW_ERR_SIG is the reference's opaque ``ed25519::Error`` (CryptoError,
+ * crypto/src/lib.rs:18) that callers map to DagError::InvalidSignature (primary/src/error.rs:27-28). */
+#define NW_OK 0
+#define NW_ERR_SIG 1
+#define NW_ERR_ARG 2
+#define NW_ERR_DEVICE 3
+#define NW_ERR_NOMEM 4
+
+/* Per-signature flag bits written by the verify kernels (nw_verify_certs sig_flags output). */
+#define NW_F_S_OK 0x001u      /* S < l (ed25519 high-bit check + dalek check_scalar) */
+#define NW_F_A_OK 0x002u      /* public key decodes (dalek::PublicKey::from_bytes) */
+#define NW_F_MATCH 0x004u     /* R decodes and R == sB - hA (strict equation holds) */
+#define NW_F_STRICT 0x008u    /* verify_strict verdict */
+#define NW_F_A_SMALL 0x010u   /* A is of small order */
+#define NW_F_R_SMALL 0x020u   /* R is of small order (meaningful when MATCH) */
+#define NW_F_SLOW 0x1000u     /* needed the exact batch equation (rare path) */
+#define NW_F_R_BAD 0x2000u    /* R failed to decode (found on the exact path) */
+
+typedef struct nw_ctx nw_ctx;
+
+typedef struct nw_opts {
+    int device;        /* HIP device ordinal (one process per GPU; -1 = current device) */
+    uint32_t flags;    /* reserved, 0 */
+    size_t max_keys;   /* committee/key-cache capacity in keys (0 = default 16384) */
+} nw_opts;
+
+/* One certificate: its votes are sig[first_vote .. first_vote + n_votes). */
+typedef struct nw_cert {
+    uint32_t first_vote;
+    uint32_t n_votes;
+} nw_cert;
+
+/* ---- context ------------------------------------------------------------------------------- */
+int nw_ctx_create(nw_ctx** out, const nw_opts* opts);
+void nw_ctx_destroy(nw_ctx* ctx);
+/* Human-readable description of the last error on this context (thread-unsafe diagnostics). */
+const char* nw_last_error(const nw_ctx* ctx);
+
+/* ---- committee / key cache -------------------------------------------------------------------
+ * Replaces the per-vote ``dalek::PublicKey::from_bytes`` decompression at crypto/src/lib.rs:216
+ * (and :202) with a one-time decompression + fixed-base table build per key.  A key that fails
+ * to decode is still cached with its failure recorded, so verification returns NW_ERR_SIG for it
+ * exactly where the reference's ``?`` would.  Returns the slot index of each key in ``slot_out``
+ * (may be NULL).  Keys already cached keep their slot. ``stake`` may be NULL (stake 0). */
+int nw_committee_load(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, size_t n,
+                      uint32_t* slot_out);
+/* Number of cached keys. */
+size_t nw_committee_size(const nw_ctx* ctx);
+
+/* ---- verification ----------------------------------------------------------------------------
+ * crypto::Signature::verify (crypto/src/lib.rs:200-204): strict single verify of ``msg``. */
+int nw_verify_strict(nw_ctx* ctx, const uint8_t* msg, size_t len, const uint8_t pk[32],
+                     const uint8_t sig[64]);
+
+/* Bulk strict verify (Header::verify / Vote::verify callers, primary/src/messages.rs:48-67,131-142):
+ * n independent (msg_i, pk_i, sig_i); ok[i] = 1 when verify_strict accepts. */
+int nw_verify_strict_many(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len,
+                          const uint8_t (*pk)[32], const uint8_t (*sig)[64], size_t n, uint8_t* ok);
+
+/* dalek::verify_batch as called by crypto::Signature::verify_batch (crypto/src/lib.rs:218) and by
+ * the worker's simulated load (worker/src/processor.rs:78): one verdict for n signatures over
+ * per-signature messages.  Coefficients: NW-Z v1 stream ``zseed`` with batch index ``batch_index``.
+ * Returns NW_OK / NW_ERR_SIG. */
+int nw_verify_batch(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len,
+                    const uint8_t (*pk)[32], const uint8_t (*sig)[64], size_t n,
+                    const uint8_t zseed[32], uint64_t batch_index);
+
+/* Certificate bulk path (Certificate::verify's batch step, primary/src/messages.rs:214, for many
+ * certificates at once).  Signers are committee slots (nw_committee_load).  msg[c] is the 32-byte
+ * certificate digest.  Outputs (each may be NULL):
+ *   cert_ok[c]        1 iff Signature::verify_batch(msg[c], votes of c) is Ok
+ *   sig_ok[v]         1 iff verify_strict accepts vote v (the per-signature fallback bitmap)
+ *   accepted_stake[c] sum of signer stake over votes with sig_ok = 1
+ * Coefficients for certificate c use batch index cert_base + c. */
+int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint8_t (*sig)[64],
+                    const uint32_t* signer_slot, const uint8_t (*msg)[32], const uint8_t zseed[32],
+                    uint64_t cert_base, uint8_t* cert_ok, uint8_t* sig_ok, uint64_t* accepted_stake);
+
+/* Device-resident variant for streaming use (inputs already in HBM).  All pointers are device
+ * pointers; ``stream`` is a hipStream_t (NULL = default stream).  Enqueues work and returns;
+ * ``sig_flags`` (uint32 per vote, NW_F_* bits) may be NULL. */
+int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first,
+                        const uint32_t* d_cert_nvotes, size_t nsigs, const uint8_t* d_sig64,
+                        const uint32_t* d_signer_slot, const uint8_t* d_msg32,
+                        const uint8_t zseed[32], uint64_t cert_base, uint8_t* d_cert_ok,
+                        uint32_t* d_sig_flags, uint64_t* d_accepted_stake, void* stream);
+
+/* ---- digests ---------------------------------------------------------------------------------
+ * sha2 0.9 Sha512 via ed25519_dalek::Sha512 (primary/src/messages.rs:72-82,147-151,228-232;
+ * worker/src/processor.rs:65; worker/src/batch_maker.rs:125).  Callers truncate to 32 bytes. */
+int nw_sha512(nw_ctx* ctx, const uint8_t* data, size_t len, uint8_t out[64]);
+int nw_sha512_many(nw_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                   size_t n, uint8_t (*out)[64]);
+/* Device-resident bulk digest: d_base/d_off/d_len/d_out are device pointers. */
+int nw_sha512_many_dev(nw_ctx* ctx, const uint8_t* d_base, const uint64_t* d_off,
+                       const uint64_t* d_len, size_t n, uint8_t* d_out64, void* stream);
+
+/* ---- signing (crypto::Signature::new / generate_keypair, crypto/src/lib.rs:163-191) -------------
+ * Low-volume in the reference; here it makes synthetic workloads.  RFC 8032 Ed25519 over
+ * messages of exactly ``msg_len`` bytes (8 or 32). pk or sig may be NULL. */
+int nw_sign_many(nw_ctx* ctx, const uint8_t (*seed)[32], const uint8_t* msgs, size_t msg_len,
+                 size_t n, uint8_t (*pk)[32], uint8_t (*sig)[64]);
+int nw_sign_many_dev(nw_ctx* ctx, const uint8_t* d_seed32, const uint8_t* d_msgs, size_t msg_len,
+                     size_t n, uint8_t* d_pk32, uint8_t* d_sig64, void* stream);
+
+/* Library build identifier (gfx target, build date). */
+const char* nw_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NWCRYPTO_H */

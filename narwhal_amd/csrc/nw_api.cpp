@@ -1,0 +1,587 @@
+// C-ABI host layer of libnwcrypto (include/nwcrypto.h): device memory, the key cache, workspace,
+// and the launch sequences.  No CPU compute path: every verdict and digest comes from the GPU.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "nw_kernels.h"
+#include "nw_point.h"
+
+using namespace nw;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <typename T>
+    T* as() const {
+        return reinterpret_cast<T*>(p);
+    }
+};
+
+}  // namespace
+
+struct nw_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::string last_error;
+    // basepoint comb
+    uint32_t* d_btab = nullptr;
+    // key cache
+    size_t max_keys = 16384;
+    size_t nkeys = 0, key_cap = 0;
+    uint32_t* d_keys_raw = nullptr;
+    uint32_t* d_key_info = nullptr;
+    uint32_t* d_stake = nullptr;
+    uint32_t* d_key_tab = nullptr;
+    std::unordered_map<std::string, uint32_t> slot_of;
+    std::vector<uint32_t> h_stake;
+    // workspace
+    DevBuf w_bases, w_sig, w_signer, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len,
+        w_flags, w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_stake_out, w_ok, w_misc,
+        w_out;
+};
+
+namespace {
+
+int fail(nw_ctx* c, hipError_t e, const char* what) {
+    if (c) {
+        c->last_error = std::string(what) + ": " + hipGetErrorString(e);
+    }
+    return e == hipErrorOutOfMemory ? NW_ERR_NOMEM : NW_ERR_DEVICE;
+}
+
+#define NW_TRY(expr, what)                              \
+    do {                                                \
+        hipError_t e_ = (expr);                         \
+        if (e_ != hipSuccess) return fail(ctx, e_, what); \
+    } while (0)
+
+// Basepoint encoding (y = 4/5, x even).
+const uint8_t kBaseEnc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                              0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                              0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
+
+int grow_keys(nw_ctx* ctx, size_t need) {
+    if (need <= ctx->key_cap) return NW_OK;
+    if (need > ctx->max_keys) {
+        ctx->last_error = "key cache capacity exceeded (nw_opts.max_keys)";
+        return NW_ERR_NOMEM;
+    }
+    size_t cap = ctx->key_cap ? ctx->key_cap : 64;
+    while (cap < need) cap *= 2;
+    if (cap > ctx->max_keys) cap = ctx->max_keys;
+    uint32_t *raw = nullptr, *info = nullptr, *stake = nullptr, *tab = nullptr;
+    NW_TRY(hipMalloc(&raw, cap * 32), "hipMalloc(keys_raw)");
+    NW_TRY(hipMalloc(&info, cap * 4), "hipMalloc(key_info)");
+    NW_TRY(hipMalloc(&stake, cap * 4), "hipMalloc(stake)");
+    NW_TRY(hipMalloc(&tab, cap * (size_t)COMB_WORDS * 4), "hipMalloc(key_tab)");
+    if (ctx->nkeys) {
+        NW_TRY(hipMemcpyAsync(raw, ctx->d_keys_raw, ctx->nkeys * 32, hipMemcpyDeviceToDevice, ctx->stream), "copy");
+        NW_TRY(hipMemcpyAsync(info, ctx->d_key_info, ctx->nkeys * 4, hipMemcpyDeviceToDevice, ctx->stream), "copy");
+        NW_TRY(hipMemcpyAsync(stake, ctx->d_stake, ctx->nkeys * 4, hipMemcpyDeviceToDevice, ctx->stream), "copy");
+        NW_TRY(hipMemcpyAsync(tab, ctx->d_key_tab, ctx->nkeys * (size_t)COMB_WORDS * 4, hipMemcpyDeviceToDevice,
+                              ctx->stream),
+               "copy");
+        NW_TRY(hipStreamSynchronize(ctx->stream), "sync");
+        (void)hipFree(ctx->d_keys_raw);
+        (void)hipFree(ctx->d_key_info);
+        (void)hipFree(ctx->d_stake);
+        (void)hipFree(ctx->d_key_tab);
+    }
+    ctx->d_keys_raw = raw;
+    ctx->d_key_info = info;
+    ctx->d_stake = stake;
+    ctx->d_key_tab = tab;
+    ctx->key_cap = cap;
+    return NW_OK;
+}
+
+// Build tables for keys [k0, k0 + nk) whose raw bytes are already in d_keys_raw.
+int build_keys(nw_ctx* ctx, uint32_t* d_raw, uint32_t* d_info, uint32_t* d_tab, size_t nk) {
+    const size_t chunk = 4096;   // bounds the bases scratch (5 KB per key)
+    for (size_t s = 0; s < nk; s += chunk) {
+        const size_t m = nk - s < chunk ? nk - s : chunk;
+        NW_TRY(ctx->w_bases.ensure(m * COMB_POS * 40 * 4), "hipMalloc(bases)");
+        NW_TRY(launch_key_prep((uint32_t)m, d_raw + s * 8, d_info + s, ctx->w_bases.as<uint32_t>(),
+                               d_tab + s * (size_t)COMB_WORDS, ctx->stream),
+               "k_key_prep/k_comb_entries");
+    }
+    return NW_OK;
+}
+
+// Map keys to cache slots, loading unknown keys (table build on the GPU).
+int ensure_slots(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, size_t n, uint32_t* slots) {
+    std::vector<uint32_t> new_idx;
+    std::vector<uint8_t> new_raw;
+    std::unordered_map<std::string, uint32_t> pending;
+    for (size_t i = 0; i < n; ++i) {
+        std::string k(reinterpret_cast<const char*>(pk[i]), 32);
+        auto it = ctx->slot_of.find(k);
+        if (it != ctx->slot_of.end()) {
+            slots[i] = it->second;
+            if (stake) {
+                ctx->h_stake[it->second] = stake[i];
+                new_idx.push_back(it->second);   // stake refresh only
+            }
+            continue;
+        }
+        auto pit = pending.find(k);
+        if (pit != pending.end()) {
+            slots[i] = pit->second;
+            continue;
+        }
+        const uint32_t slot = (uint32_t)(ctx->nkeys + pending.size());
+        pending.emplace(k, slot);
+        slots[i] = slot;
+        new_raw.insert(new_raw.end(), pk[i], pk[i] + 32);
+        ctx->h_stake.push_back(stake ? stake[i] : 0u);
+    }
+    const size_t add = pending.size();
+    if (add) {
+        int rc = grow_keys(ctx, ctx->nkeys + add);
+        if (rc != NW_OK) {
+            ctx->h_stake.resize(ctx->nkeys);
+            return rc;
+        }
+        const size_t k0 = ctx->nkeys;
+        NW_TRY(hipMemcpyAsync(ctx->d_keys_raw + k0 * 8, new_raw.data(), add * 32, hipMemcpyHostToDevice, ctx->stream),
+               "H2D keys");
+        rc = build_keys(ctx, ctx->d_keys_raw + k0 * 8, ctx->d_key_info + k0, ctx->d_key_tab + k0 * (size_t)COMB_WORDS,
+                        add);
+        if (rc != NW_OK) return rc;
+        for (auto& kv : pending) ctx->slot_of.emplace(kv.first, kv.second);
+        ctx->nkeys += add;
+    }
+    if (add || !new_idx.empty()) {
+        NW_TRY(hipMemcpyAsync(ctx->d_stake, ctx->h_stake.data(), ctx->nkeys * 4, hipMemcpyHostToDevice, ctx->stream),
+               "H2D stake");
+        NW_TRY(hipStreamSynchronize(ctx->stream), "sync(committee)");
+    }
+    return NW_OK;
+}
+
+void fill_zseed(uint32_t out[8], const uint8_t* zseed) {
+    if (!zseed) {
+        for (int k = 0; k < 8; ++k) out[k] = 0;
+        return;
+    }
+    std::memcpy(out, zseed, 32);
+}
+
+// Enqueue the certificate pipeline on device buffers.
+int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uint32_t* d_nv, size_t nsigs,
+                  const uint8_t* d_sig, const uint32_t* d_signer, int msgmode, const uint8_t* d_msg32,
+                  const uint8_t* d_msg_base, const uint64_t* d_msg_off, const uint64_t* d_msg_len,
+                  const uint8_t* zseed, uint64_t cert_base, uint32_t batch_mode, uint8_t* d_cert_ok,
+                  uint32_t* d_flags_user, uint64_t* d_stake_out, hipStream_t st) {
+    uint32_t* d_flags = d_flags_user;
+    if (!d_flags) {
+        NW_TRY(ctx->w_flags.ensure(nsigs * 4 + 4), "ws flags");
+        d_flags = ctx->w_flags.as<uint32_t>();
+    }
+    NW_TRY(ctx->w_sig_cert.ensure(nsigs * 4 + 4), "ws sig_cert");
+    NW_TRY(ctx->w_slow_count.ensure(16), "ws slow_count");
+    NW_TRY(ctx->w_slow_list.ensure(nsigs * 4 + 4), "ws slow_list");
+    NW_TRY(ctx->w_slow_slot.ensure(nsigs * 4 + 4), "ws slow_slot");
+    if (batch_mode) NW_TRY(ctx->w_slow_buf.ensure(nsigs * (size_t)SLOW_WORDS * 4 + 4), "ws slow_buf");
+    NW_TRY(hipMemsetAsync(ctx->w_slow_count.p, 0, 16, st), "memset");
+    NW_TRY(launch_expand_certs((uint32_t)ncerts, d_first, d_nv, ctx->w_sig_cert.as<uint32_t>(), st), "k_expand_certs");
+
+    VerifyParams vp{};
+    vp.n = (uint32_t)nsigs;
+    vp.batch_mode = batch_mode;
+    vp.sig = d_sig;
+    vp.signer = d_signer;
+    vp.sig_cert = ctx->w_sig_cert.as<uint32_t>();
+    vp.cert_first = d_first;
+    vp.cert_msg = d_msg32;
+    vp.msg_base = d_msg_base;
+    vp.msg_off = d_msg_off;
+    vp.msg_len = d_msg_len;
+    vp.cert_base = cert_base;
+    vp.keys_raw = ctx->d_keys_raw;
+    vp.key_info = ctx->d_key_info;
+    vp.key_tab = ctx->d_key_tab;
+    vp.btab = ctx->d_btab;
+    fill_zseed(vp.zseed, zseed);
+    vp.flags = d_flags;
+    vp.slow_count = ctx->w_slow_count.as<uint32_t>();
+    vp.slow_list = ctx->w_slow_list.as<uint32_t>();
+    vp.slow_slot = ctx->w_slow_slot.as<uint32_t>();
+    vp.slow_buf = ctx->w_slow_buf.as<uint32_t>();
+    NW_TRY(launch_verify(vp, msgmode, st), "k_verify");
+    if (!batch_mode) return NW_OK;
+
+    SlowParams sp{};
+    sp.slow_count = vp.slow_count;
+    sp.slow_list = vp.slow_list;
+    sp.slow_buf = vp.slow_buf;
+    sp.sig = d_sig;
+    sp.flags = d_flags;
+    NW_TRY(launch_slow(sp, (uint32_t)nsigs, st), "k_slow_sig");
+
+    FinalizeParams fp{};
+    fp.ncerts = (uint32_t)ncerts;
+    fp.cert_first = d_first;
+    fp.cert_n = d_nv;
+    fp.flags = d_flags;
+    fp.signer = d_signer;
+    fp.stake = ctx->d_stake;
+    fp.slow_slot = vp.slow_slot;
+    fp.slow_buf = vp.slow_buf;
+    fp.cert_ok = d_cert_ok;
+    fp.accepted_stake = d_stake_out;
+    NW_TRY(launch_finalize(fp, st), "k_cert_finalize");
+    return NW_OK;
+}
+
+// Pack per-signature messages into one device buffer (MSGMODE 1).
+int upload_messages(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, size_t n) {
+    std::vector<uint64_t> off(n), ln(n);
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        off[i] = total;
+        ln[i] = len[i];
+        total += len[i];
+    }
+    std::vector<uint8_t> packed(total + 8);
+    for (size_t i = 0; i < n; ++i)
+        if (len[i]) std::memcpy(packed.data() + off[i], msg[i], len[i]);
+    NW_TRY(ctx->w_msg.ensure(total + 8), "ws msg");
+    NW_TRY(ctx->w_msg_off.ensure(n * 8 + 8), "ws msg_off");
+    NW_TRY(ctx->w_msg_len.ensure(n * 8 + 8), "ws msg_len");
+    NW_TRY(hipMemcpyAsync(ctx->w_msg.p, packed.data(), total + 8, hipMemcpyHostToDevice, ctx->stream), "H2D msg");
+    NW_TRY(hipMemcpyAsync(ctx->w_msg_off.p, off.data(), n * 8, hipMemcpyHostToDevice, ctx->stream), "H2D off");
+    NW_TRY(hipMemcpyAsync(ctx->w_msg_len.p, ln.data(), n * 8, hipMemcpyHostToDevice, ctx->stream), "H2D len");
+    return NW_OK;
+}
+
+// Shared body of strict_many / verify_batch: every signature in one "certificate" 0.
+int run_generic(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const uint8_t (*pk)[32],
+                const uint8_t (*sig)[64], size_t n, const uint8_t* zseed, uint64_t batch_index, uint32_t batch_mode,
+                uint8_t* ok_out, uint8_t* verdict_out) {
+    std::vector<uint32_t> slots(n);
+    int rc = ensure_slots(ctx, pk, nullptr, n, slots.data());
+    if (rc != NW_OK) return rc;
+    rc = upload_messages(ctx, msg, len, n);
+    if (rc != NW_OK) return rc;
+    NW_TRY(ctx->w_sig.ensure(n * 64), "ws sig");
+    NW_TRY(ctx->w_signer.ensure(n * 4), "ws signer");
+    NW_TRY(ctx->w_cert_first.ensure(16), "ws first");
+    NW_TRY(ctx->w_cert_n.ensure(16), "ws n");
+    NW_TRY(ctx->w_cert_ok.ensure(16), "ws cert_ok");
+    NW_TRY(ctx->w_ok.ensure(n + 16), "ws ok");
+    const uint32_t first = 0, nv = (uint32_t)n;
+    NW_TRY(hipMemcpyAsync(ctx->w_sig.p, sig, n * 64, hipMemcpyHostToDevice, ctx->stream), "H2D sig");
+    NW_TRY(hipMemcpyAsync(ctx->w_signer.p, slots.data(), n * 4, hipMemcpyHostToDevice, ctx->stream), "H2D signer");
+    NW_TRY(hipMemcpyAsync(ctx->w_cert_first.p, &first, 4, hipMemcpyHostToDevice, ctx->stream), "H2D first");
+    NW_TRY(hipMemcpyAsync(ctx->w_cert_n.p, &nv, 4, hipMemcpyHostToDevice, ctx->stream), "H2D n");
+    rc = enqueue_certs(ctx, 1, ctx->w_cert_first.as<uint32_t>(), ctx->w_cert_n.as<uint32_t>(), n,
+                       ctx->w_sig.as<uint8_t>(), ctx->w_signer.as<uint32_t>(), 1, nullptr, ctx->w_msg.as<uint8_t>(),
+                       ctx->w_msg_off.as<uint64_t>(), ctx->w_msg_len.as<uint64_t>(), zseed, batch_index, batch_mode,
+                       ctx->w_cert_ok.as<uint8_t>(), nullptr, nullptr, ctx->stream);
+    if (rc != NW_OK) return rc;
+    if (ok_out) {
+        NW_TRY(launch_flags_to_ok((uint32_t)n, ctx->w_flags.as<uint32_t>(), ctx->w_ok.as<uint8_t>(), ctx->stream),
+               "k_flags_to_ok");
+        NW_TRY(hipMemcpyAsync(ok_out, ctx->w_ok.p, n, hipMemcpyDeviceToHost, ctx->stream), "D2H ok");
+    }
+    if (verdict_out) NW_TRY(hipMemcpyAsync(verdict_out, ctx->w_cert_ok.p, 1, hipMemcpyDeviceToHost, ctx->stream), "D2H");
+    NW_TRY(hipStreamSynchronize(ctx->stream), "sync");
+    return NW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nw_version(void) { return "nwcrypto 0.1 gfx950 " __DATE__; }
+
+int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
+    if (!out) return NW_ERR_ARG;
+    *out = nullptr;
+    nw_ctx* ctx = new nw_ctx();
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev == 0) {
+        delete ctx;
+        return NW_ERR_DEVICE;
+    }
+    int dev = opts && opts->device >= 0 ? opts->device : -1;
+    if (dev < 0) {
+        e = hipGetDevice(&dev);
+        if (e != hipSuccess) {
+            delete ctx;
+            return NW_ERR_DEVICE;
+        }
+    }
+    if (dev >= ndev) {
+        delete ctx;
+        return NW_ERR_ARG;
+    }
+    ctx->device = dev;
+    if (opts && opts->max_keys) ctx->max_keys = opts->max_keys;
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return NW_ERR_DEVICE;
+    }
+    // basepoint comb (one "key" = B)
+    uint32_t* d_braw = nullptr;
+    uint32_t* d_binfo = nullptr;
+    if (hipMalloc(&ctx->d_btab, (size_t)COMB_WORDS * 4) != hipSuccess || hipMalloc(&d_braw, 32) != hipSuccess ||
+        hipMalloc(&d_binfo, 16) != hipSuccess) {
+        nw_ctx_destroy(ctx);
+        return NW_ERR_NOMEM;
+    }
+    int rc = NW_OK;
+    if (hipMemcpy(d_braw, kBaseEnc, 32, hipMemcpyHostToDevice) != hipSuccess) rc = NW_ERR_DEVICE;
+    if (rc == NW_OK) rc = build_keys(ctx, d_braw, d_binfo, ctx->d_btab, 1);
+    if (rc == NW_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = NW_ERR_DEVICE;
+    (void)hipFree(d_braw);
+    (void)hipFree(d_binfo);
+    if (rc != NW_OK) {
+        nw_ctx_destroy(ctx);
+        return rc;
+    }
+    *out = ctx;
+    return NW_OK;
+}
+
+void nw_ctx_destroy(nw_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    for (DevBuf* b : {&ctx->w_bases, &ctx->w_sig, &ctx->w_signer, &ctx->w_sig_cert, &ctx->w_cert_first, &ctx->w_cert_n,
+                      &ctx->w_msg, &ctx->w_msg_off, &ctx->w_msg_len, &ctx->w_flags, &ctx->w_slow_count,
+                      &ctx->w_slow_list, &ctx->w_slow_slot, &ctx->w_slow_buf, &ctx->w_cert_ok, &ctx->w_stake_out,
+                      &ctx->w_ok, &ctx->w_misc, &ctx->w_out})
+        b->release();
+    for (uint32_t* p : {ctx->d_btab, ctx->d_keys_raw, ctx->d_key_info, ctx->d_stake, ctx->d_key_tab})
+        if (p) (void)hipFree(p);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char* nw_last_error(const nw_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+size_t nw_committee_size(const nw_ctx* ctx) { return ctx ? ctx->nkeys : 0; }
+
+int nw_committee_load(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, size_t n, uint32_t* slot_out) {
+    if (!ctx || (!pk && n)) return NW_ERR_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    std::vector<uint32_t> slots(n);
+    int rc = ensure_slots(ctx, pk, stake, n, slots.data());
+    if (rc == NW_OK && slot_out) std::memcpy(slot_out, slots.data(), n * 4);
+    return rc;
+}
+
+int nw_verify_strict_many(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const uint8_t (*pk)[32],
+                          const uint8_t (*sig)[64], size_t n, uint8_t* ok) {
+    if (!ctx || !ok || (n && (!msg || !len || !pk || !sig))) return NW_ERR_ARG;
+    if (n == 0) return NW_OK;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    return run_generic(ctx, msg, len, pk, sig, n, nullptr, 0, 0, ok, nullptr);
+}
+
+int nw_verify_strict(nw_ctx* ctx, const uint8_t* msg, size_t len, const uint8_t pk[32], const uint8_t sig[64]) {
+    if (!ctx || !pk || !sig || (len && !msg)) return NW_ERR_ARG;
+    uint8_t ok = 0;
+    const uint8_t* m = msg ? msg : reinterpret_cast<const uint8_t*>("");
+    int rc = nw_verify_strict_many(ctx, &m, &len, reinterpret_cast<const uint8_t(*)[32]>(pk),
+                                   reinterpret_cast<const uint8_t(*)[64]>(sig), 1, &ok);
+    if (rc != NW_OK) return rc;
+    return ok ? NW_OK : NW_ERR_SIG;
+}
+
+int nw_verify_batch(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const uint8_t (*pk)[32],
+                    const uint8_t (*sig)[64], size_t n, const uint8_t zseed[32], uint64_t batch_index) {
+    if (!ctx || (n && (!msg || !len || !pk || !sig))) return NW_ERR_ARG;
+    if (n == 0) return NW_OK;   // empty batch: the MSM is (-0)B = identity -> Ok
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    uint8_t verdict = 0;
+    int rc = run_generic(ctx, msg, len, pk, sig, n, zseed, batch_index, 1, nullptr, &verdict);
+    if (rc != NW_OK) return rc;
+    return verdict ? NW_OK : NW_ERR_SIG;
+}
+
+int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint8_t (*sig)[64],
+                    const uint32_t* signer_slot, const uint8_t (*msg)[32], const uint8_t zseed[32], uint64_t cert_base,
+                    uint8_t* cert_ok, uint8_t* sig_ok, uint64_t* accepted_stake) {
+    if (!ctx || (ncerts && (!certs || !msg))) return NW_ERR_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    size_t nsigs = 0;
+    std::vector<uint32_t> first(ncerts), nv(ncerts);
+    for (size_t c = 0; c < ncerts; ++c) {
+        first[c] = certs[c].first_vote;
+        nv[c] = certs[c].n_votes;
+        const size_t end = (size_t)certs[c].first_vote + certs[c].n_votes;
+        if (end > nsigs) nsigs = end;
+    }
+    if (nsigs && (!sig || !signer_slot)) return NW_ERR_ARG;
+    for (size_t v = 0; v < nsigs; ++v)
+        if (signer_slot[v] >= ctx->nkeys) {
+            ctx->last_error = "signer slot out of range (load the committee first)";
+            return NW_ERR_ARG;
+        }
+    NW_TRY(ctx->w_sig.ensure(nsigs * 64 + 64), "ws sig");
+    NW_TRY(ctx->w_signer.ensure(nsigs * 4 + 4), "ws signer");
+    NW_TRY(ctx->w_cert_first.ensure(ncerts * 4 + 4), "ws first");
+    NW_TRY(ctx->w_cert_n.ensure(ncerts * 4 + 4), "ws n");
+    NW_TRY(ctx->w_msg.ensure(ncerts * 32 + 32), "ws msg");
+    NW_TRY(ctx->w_cert_ok.ensure(ncerts + 16), "ws cert_ok");
+    NW_TRY(ctx->w_stake_out.ensure(ncerts * 8 + 8), "ws stake");
+    NW_TRY(ctx->w_ok.ensure(nsigs + 16), "ws ok");
+    hipStream_t st = ctx->stream;
+    if (nsigs) {
+        NW_TRY(hipMemcpyAsync(ctx->w_sig.p, sig, nsigs * 64, hipMemcpyHostToDevice, st), "H2D sig");
+        NW_TRY(hipMemcpyAsync(ctx->w_signer.p, signer_slot, nsigs * 4, hipMemcpyHostToDevice, st), "H2D signer");
+    }
+    if (ncerts) {
+        NW_TRY(hipMemcpyAsync(ctx->w_cert_first.p, first.data(), ncerts * 4, hipMemcpyHostToDevice, st), "H2D first");
+        NW_TRY(hipMemcpyAsync(ctx->w_cert_n.p, nv.data(), ncerts * 4, hipMemcpyHostToDevice, st), "H2D n");
+        NW_TRY(hipMemcpyAsync(ctx->w_msg.p, msg, ncerts * 32, hipMemcpyHostToDevice, st), "H2D msg");
+    }
+    int rc = enqueue_certs(ctx, ncerts, ctx->w_cert_first.as<uint32_t>(), ctx->w_cert_n.as<uint32_t>(), nsigs,
+                           ctx->w_sig.as<uint8_t>(), ctx->w_signer.as<uint32_t>(), 0, ctx->w_msg.as<uint8_t>(), nullptr,
+                           nullptr, nullptr, zseed, cert_base, 1, ctx->w_cert_ok.as<uint8_t>(), nullptr,
+                           ctx->w_stake_out.as<uint64_t>(), st);
+    if (rc != NW_OK) return rc;
+    if (sig_ok && nsigs) {
+        NW_TRY(launch_flags_to_ok((uint32_t)nsigs, ctx->w_flags.as<uint32_t>(), ctx->w_ok.as<uint8_t>(), st),
+               "k_flags_to_ok");
+        NW_TRY(hipMemcpyAsync(sig_ok, ctx->w_ok.p, nsigs, hipMemcpyDeviceToHost, st), "D2H sig_ok");
+    }
+    if (cert_ok && ncerts) NW_TRY(hipMemcpyAsync(cert_ok, ctx->w_cert_ok.p, ncerts, hipMemcpyDeviceToHost, st), "D2H");
+    if (accepted_stake && ncerts)
+        NW_TRY(hipMemcpyAsync(accepted_stake, ctx->w_stake_out.p, ncerts * 8, hipMemcpyDeviceToHost, st), "D2H");
+    NW_TRY(hipStreamSynchronize(st), "sync");
+    return NW_OK;
+}
+
+int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first, const uint32_t* d_cert_nvotes,
+                        size_t nsigs, const uint8_t* d_sig64, const uint32_t* d_signer_slot, const uint8_t* d_msg32,
+                        const uint8_t zseed[32], uint64_t cert_base, uint8_t* d_cert_ok, uint32_t* d_sig_flags,
+                        uint64_t* d_accepted_stake, void* stream) {
+    if (!ctx) return NW_ERR_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    return enqueue_certs(ctx, ncerts, d_cert_first, d_cert_nvotes, nsigs, d_sig64, d_signer_slot, 0, d_msg32, nullptr,
+                         nullptr, nullptr, zseed, cert_base, 1, d_cert_ok, d_sig_flags, d_accepted_stake,
+                         reinterpret_cast<hipStream_t>(stream));
+}
+
+int nw_sha512_many_dev(nw_ctx* ctx, const uint8_t* d_base, const uint64_t* d_off, const uint64_t* d_len, size_t n,
+                       uint8_t* d_out64, void* stream) {
+    if (!ctx) return NW_ERR_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    NW_TRY(launch_sha512_many((uint32_t)n, d_base, d_off, d_len, d_out64, reinterpret_cast<hipStream_t>(stream)),
+           "k_sha512_many");
+    return NW_OK;
+}
+
+int nw_sha512_many(nw_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint64_t* len, size_t n,
+                   uint8_t (*out)[64]) {
+    if (!ctx || (n && (!off || !len || !out))) return NW_ERR_ARG;
+    if (n == 0) return NW_OK;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    // upload only the referenced span
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (off[i] < lo) lo = off[i];
+        if (off[i] + len[i] > hi) hi = off[i] + len[i];
+    }
+    if (hi < lo) hi = lo;
+    std::vector<uint64_t> roff(n);
+    for (size_t i = 0; i < n; ++i) roff[i] = off[i] - lo;
+    const size_t span = (size_t)(hi - lo);
+    hipStream_t st = ctx->stream;
+    NW_TRY(ctx->w_msg.ensure(span + 16), "ws msg");
+    NW_TRY(ctx->w_msg_off.ensure(n * 8), "ws off");
+    NW_TRY(ctx->w_msg_len.ensure(n * 8), "ws len");
+    NW_TRY(ctx->w_out.ensure(n * 64), "ws out");
+    if (span) NW_TRY(hipMemcpyAsync(ctx->w_msg.p, base + lo, span, hipMemcpyHostToDevice, st), "H2D data");
+    NW_TRY(hipMemcpyAsync(ctx->w_msg_off.p, roff.data(), n * 8, hipMemcpyHostToDevice, st), "H2D off");
+    NW_TRY(hipMemcpyAsync(ctx->w_msg_len.p, len, n * 8, hipMemcpyHostToDevice, st), "H2D len");
+    NW_TRY(launch_sha512_many((uint32_t)n, ctx->w_msg.as<uint8_t>(), ctx->w_msg_off.as<uint64_t>(),
+                              ctx->w_msg_len.as<uint64_t>(), ctx->w_out.as<uint8_t>(), st),
+           "k_sha512_many");
+    NW_TRY(hipMemcpyAsync(out, ctx->w_out.p, n * 64, hipMemcpyDeviceToHost, st), "D2H digests");
+    NW_TRY(hipStreamSynchronize(st), "sync");
+    return NW_OK;
+}
+
+int nw_sha512(nw_ctx* ctx, const uint8_t* data, size_t len, uint8_t out[64]) {
+    const uint64_t off = 0, ln = len;
+    static const uint8_t empty[1] = {0};
+    return nw_sha512_many(ctx, data ? data : empty, &off, &ln, 1, reinterpret_cast<uint8_t(*)[64]>(out));
+}
+
+int nw_sign_many_dev(nw_ctx* ctx, const uint8_t* d_seed32, const uint8_t* d_msgs, size_t msg_len, size_t n,
+                     uint8_t* d_pk32, uint8_t* d_sig64, void* stream) {
+    if (!ctx || (msg_len != 8 && msg_len != 32)) return NW_ERR_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    NW_TRY(launch_sign((uint32_t)n, (int)(msg_len / 4), reinterpret_cast<const uint32_t*>(d_seed32),
+                       reinterpret_cast<const uint32_t*>(d_msgs), ctx->d_btab, reinterpret_cast<uint32_t*>(d_pk32),
+                       reinterpret_cast<uint32_t*>(d_sig64), reinterpret_cast<hipStream_t>(stream)),
+           "k_sign");
+    return NW_OK;
+}
+
+int nw_sign_many(nw_ctx* ctx, const uint8_t (*seed)[32], const uint8_t* msgs, size_t msg_len, size_t n,
+                 uint8_t (*pk)[32], uint8_t (*sig)[64]) {
+    if (!ctx || (msg_len != 8 && msg_len != 32) || (n && (!seed || !msgs))) return NW_ERR_ARG;
+    if (n == 0) return NW_OK;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t st = ctx->stream;
+    NW_TRY(ctx->w_misc.ensure(n * 32 + n * msg_len + 16), "ws misc");
+    NW_TRY(ctx->w_out.ensure(n * 96 + 16), "ws out");
+    uint8_t* d_seed = ctx->w_misc.as<uint8_t>();
+    uint8_t* d_msg = d_seed + n * 32;
+    uint8_t* d_pk = ctx->w_out.as<uint8_t>();
+    uint8_t* d_sig = d_pk + n * 32;
+    NW_TRY(hipMemcpyAsync(d_seed, seed, n * 32, hipMemcpyHostToDevice, st), "H2D seed");
+    NW_TRY(hipMemcpyAsync(d_msg, msgs, n * msg_len, hipMemcpyHostToDevice, st), "H2D msg");
+    NW_TRY(launch_sign((uint32_t)n, (int)(msg_len / 4), reinterpret_cast<const uint32_t*>(d_seed),
+                       reinterpret_cast<const uint32_t*>(d_msg), ctx->d_btab, reinterpret_cast<uint32_t*>(d_pk),
+                       reinterpret_cast<uint32_t*>(d_sig), st),
+           "k_sign");
+    if (pk) NW_TRY(hipMemcpyAsync(pk, d_pk, n * 32, hipMemcpyDeviceToHost, st), "D2H pk");
+    if (sig) NW_TRY(hipMemcpyAsync(sig, d_sig, n * 64, hipMemcpyDeviceToHost, st), "D2H sig");
+    NW_TRY(hipStreamSynchronize(st), "sync");
+    return NW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,306 @@
+// Per-lane building blocks of the verify / sign kernels, shared with the test-only host harness
+// (tools/hostcheck.hip) so the exact code the GPU runs is unit-tested against the oracle.
+#pragma once
+#include "nw_point.h"
+#include "nw_sha512.h"
+#include "nw_chacha.h"
+#include "nw_kernels.h"
+
+namespace nw {
+
+// ------------------------------------------------------------------------------------ loads
+NW_HD void load_w8(uint32_t w[8], const uint32_t* p) {
+    const uint4 a = reinterpret_cast<const uint4*>(p)[0];
+    const uint4 b = reinterpret_cast<const uint4*>(p)[1];
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+NW_HD ge_precomp load_precomp(const uint32_t* p) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+    uint32_t w[32];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint4 t = q[k];
+        w[4 * k] = t.x; w[4 * k + 1] = t.y; w[4 * k + 2] = t.z; w[4 * k + 3] = t.w;
+    }
+    return ge_precomp_from_words(w);
+}
+
+NW_HD void store_p3(uint32_t* dst, const ge_p3& p) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        dst[k] = p.X.v[k];
+        dst[10 + k] = p.Y.v[k];
+        dst[20 + k] = p.Z.v[k];
+        dst[30 + k] = p.T.v[k];
+    }
+}
+
+NW_HD ge_p3 load_p3(const uint32_t* src) {
+    ge_p3 p;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        p.X.v[k] = src[k];
+        p.Y.v[k] = src[10 + k];
+        p.Z.v[k] = src[20 + k];
+        p.T.v[k] = src[30 + k];
+    }
+    return p;
+}
+
+// Byte of the virtual hram stream (R || A || M) at position pos >= 64, with SHA padding.
+NW_HD uint32_t stream_byte(const uint8_t* msg, uint64_t len, uint64_t pos) {
+    const uint64_t m = pos - 64;
+    if (m < len) return msg[m];
+    return m == len ? 0x80u : 0u;
+}
+
+NW_HD uint64_t stream_word(const uint8_t* msg, uint64_t len, uint64_t pos) {
+    uint64_t w = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) w = (w << 8) | stream_byte(msg, len, pos + j);
+    return w;
+}
+
+// SHA-512(R || A || msg[0..len)) for an arbitrary-length message.
+NW_HD void hram_generic(uint32_t out[16], const uint32_t R[8], const uint32_t A[8],
+                             const uint8_t* msg, uint64_t len) {
+    const uint64_t total = 64 + len;
+    const uint64_t nblocks = (total + 17 + 127) / 128;
+    uint64_t st[8];
+    sha512_init(st);
+    uint64_t w[16];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[k] = be64_from_le32(R[2 * k], R[2 * k + 1]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[4 + k] = be64_from_le32(A[2 * k], A[2 * k + 1]);
+#pragma unroll
+    for (int k = 8; k < 16; ++k) w[k] = stream_word(msg, len, 8 * k);
+    if (nblocks == 1) {
+        w[14] = 0;
+        w[15] = total * 8;
+    }
+    sha512_compress(st, w);
+    for (uint64_t b = 1; b < nblocks; ++b) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = stream_word(msg, len, b * 128 + 8 * k);
+        if (b == nblocks - 1) {
+            w[14] = 0;
+            w[15] = total * 8;
+        }
+        sha512_compress(st, w);
+    }
+    sha512_digest_le32(out, st);
+}
+
+// P = s B - h A via two signed radix-2^8 combs (32 positions each).
+template <bool WITH_A>
+NW_HD ge_p3 comb_sB_minus_hA(const uint32_t s_in[8], const uint32_t h_in[8],
+                                                  const uint32_t* __restrict__ btab,
+                                                  const uint32_t* __restrict__ atab) {
+    uint32_t s[8], h[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        s[k] = s_in[k];
+        h[k] = h_in[k];
+    }
+    int cs = 0, ch = 0;
+    ge_p3 P = ge_identity();
+#pragma nounroll
+    for (int pos = 0; pos < COMB_POS; ++pos) {
+        const int ds = next_digit256(s, cs);
+        const int as = ds < 0 ? -ds : ds;
+        const ge_precomp eb = load_precomp(btab + (size_t)(pos * COMB_ENT + as) * PRECOMP_WORDS);
+        if (WITH_A) {
+            const int dh = next_digit256(h, ch);
+            const int ah = dh < 0 ? -dh : dh;
+            const ge_precomp ea = load_precomp(atab + (size_t)(pos * COMB_ENT + ah) * PRECOMP_WORDS);
+            P = ge_madd(P, ge_precomp_cneg(eb, ds < 0));
+            P = ge_madd(P, ge_precomp_cneg(ea, dh > 0));   // -h A: negate for positive digits
+        } else {
+            P = ge_madd(P, ge_precomp_cneg(eb, ds < 0));
+        }
+    }
+    return P;
+}
+
+// h = SHA-512(R || A || M) mod l for a 32-byte message (certificate / vote digest): one block.
+NW_HD void hram_msg32(uint32_t h[8], const uint32_t R[8], const uint32_t A[8], const uint32_t M[8]) {
+    uint32_t m[24];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        m[k] = R[k];
+        m[8 + k] = A[k];
+        m[16 + k] = M[k];
+    }
+    uint32_t hw[16];
+    sha512_oneblock_le32<24>(hw, m);
+    sc_reduce512(h, hw);
+}
+
+// P = s B - h A (s forced to 0 when non-canonical so the comb's digit range stays valid).
+NW_HD ge_p3 compute_P(const uint32_t S[8], const uint32_t h[8], bool sok, const uint32_t* btab,
+                      const uint32_t* atab) {
+    uint32_t s_use[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s_use[k] = sok ? S[k] : 0u;
+    return comb_sB_minus_hA<true>(s_use, h, btab, atab);
+}
+
+// Flags from P (with zi = 1/Z_P) against the signature's R encoding:
+//   MATCH  <=> R decodes (dalek decompress) and decode(R) == P  (the strict equation R = sB - hA)
+//   STRICT <=> verify_strict accepts (adds: S ok, A ok, neither R nor A of small order)
+NW_HD uint32_t match_flags(const ge_p3& P, const fe& zi, const uint32_t R[8], bool sok, bool aok, bool asmall) {
+    uint32_t xw[8], yw[8];
+    fe_tobytes_w(xw, fe_mul(P.X, zi));
+    fe_tobytes_w(yw, fe_mul(P.Y, zi));
+    // R's y (bit 255 cleared) reduced mod p, as FieldElement::from_bytes reads it
+    uint32_t yr[8];
+    fe_tobytes_w(yr, fe_frombytes_w(R));
+    const bool x_zero = (xw[0] | xw[1] | xw[2] | xw[3] | xw[4] | xw[5] | xw[6] | xw[7]) == 0;
+    const bool match = words_eq8(yw, yr) && (x_zero || ((xw[0] & 1u) == (R[7] >> 31)));
+    const bool rsmall = y_is_small_order(yw);
+    const bool strict = sok && aok && match && !asmall && !rsmall;
+    return (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | (match ? NW_F_MATCH : 0u) |
+           (strict ? NW_F_STRICT : 0u) | (asmall ? NW_F_A_SMALL : 0u) | (rsmall ? NW_F_R_SMALL : 0u);
+}
+
+// Torsion coefficient of signature i: ((r - z h) mod 8) * t mod 8 with r = z h mod l
+// (the -5 q_i A_i^t term of the exact batch decomposition; A_i^t = t T8).
+NW_HD uint32_t torsion_coef(const uint32_t z4[4], const uint32_t h[8], uint32_t t) {
+    uint32_t z8[8] = {z4[0], z4[1], z4[2], z4[3], 0u, 0u, 0u, 0u};
+    uint32_t r[8];
+    sc_mul(r, z8, h);
+    const uint32_t zh0 = (z4[0] * h[0]) & 7u;
+    return (((r[0] - zh0) & 7u) * t) & 7u;
+}
+
+// Q_i = z_i (R_i - P_i) for a signature whose strict equation fails.
+NW_HD ge_p3 slow_term(const ge_p3& Rp, const ge_p3& P, const uint32_t z4[4]) {
+    const ge_p3 D = ge_add(Rp, ge_cached_neg(ge_to_cached(P)));
+    return ge_scalarmult_vartime<4>(z4, D);
+}
+
+// Generator T8 of the (cyclic) 8-torsion subgroup E[8].
+NW_HD ge_p3 ge_t8() {
+    ge_p3 T8;
+    T8.X = fe_from_const(FE_T8X);
+    T8.Y = fe_from_const(FE_T8Y);
+    T8.Z = fe_one();
+    T8.T = fe_mul(T8.X, T8.Y);
+    return T8;
+}
+
+// Key cache preparation for one key: returns key_info bits and writes the 32 comb bases
+// 256^pos * A (extended, 40 words each).  Undecodable keys use the identity (their verdicts are
+// Err regardless) so every table entry stays a valid curve point.
+NW_HD uint32_t key_prep_one(const uint32_t* raw, uint32_t* bases) {
+    uint32_t w[8];
+    load_w8(w, raw);
+    ge_p3 A;
+    const bool ok = ge_decompress(A, w);
+    if (!ok) A = ge_identity();
+    const ge_p3 A8 = ge_dbl(ge_dbl(ge_dbl(A)));
+    const bool small = ge_is_identity(A8);
+    const ge_p3 At = ge_scalarmult_vartime<8>(SC_5L, A);
+    const ge_cached t8c = ge_to_cached(ge_t8());
+    ge_p3 Q = ge_identity();
+    uint32_t t = 0;
+    for (uint32_t k = 0; k < 8; ++k) {
+        if (ge_eq(Q, At)) t = k;
+        Q = ge_add(Q, t8c);
+    }
+    ge_p3 cur = A;
+    for (int pos = 0; pos < COMB_POS; ++pos) {
+        store_p3(bases + (size_t)pos * 40, cur);
+        for (int d = 0; d < 8; ++d) cur = ge_dbl(cur);
+    }
+    return (ok ? KI_OK : 0u) | (small ? KI_SMALL : 0u) | (t << KI_TORSION_SHIFT);
+}
+
+// Comb entry e (0..128) of position pos: e * 256^pos * A in affine Niels form.
+NW_HD void comb_entry_one(const uint32_t* bases, uint32_t pos, uint32_t e, uint32_t* tab) {
+    ge_precomp q;
+    if (e == 0) {
+        q = ge_precomp_identity();
+    } else {
+        const ge_p3 base = load_p3(bases + (size_t)pos * 40);
+        const ge_cached bc = ge_to_cached(base);
+        ge_p3 acc = ge_identity();
+        for (int b = 7; b >= 0; --b) {
+            acc = ge_dbl(acc);
+            if ((e >> b) & 1u) acc = ge_add(acc, bc);
+        }
+        q = ge_to_precomp(acc);
+    }
+    uint32_t* dst = tab + (size_t)(pos * COMB_ENT + e) * PRECOMP_WORDS;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        dst[k] = q.ypx.v[k];
+        dst[10 + k] = q.ymx.v[k];
+        dst[20 + k] = q.xy2d.v[k];
+    }
+    dst[30] = 0;
+    dst[31] = 0;
+}
+
+// RFC 8032 Ed25519 signing of an MW-word message (crypto::Signature::new, crypto/src/lib.rs:185-191).
+template <int MW>
+NW_HD void sign_one(const uint32_t* seed_in, const uint32_t* msg_in, const uint32_t* btab, uint32_t pk[8],
+                    uint32_t sig[16]) {
+    uint32_t seed[8], m[MW];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) seed[k] = seed_in[k];
+#pragma unroll
+    for (int k = 0; k < MW; ++k) m[k] = msg_in[k];
+    uint32_t hs[16];
+    sha512_oneblock_le32<8>(hs, seed);
+    uint32_t a[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] = hs[k];
+    a[0] &= 0xFFFFFFF8u;
+    a[7] &= 0x7FFFFFFFu;
+    a[7] |= 0x40000000u;
+    uint32_t wide[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) wide[k] = k < 8 ? a[k] : 0u;
+    uint32_t ared[8];
+    sc_reduce512(ared, wide);
+    uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t Aw[8];
+    ge_compress_w(Aw, comb_sB_minus_hA<false>(ared, zero8, btab, nullptr));
+    uint32_t pm[8 + MW];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pm[k] = hs[8 + k];
+#pragma unroll
+    for (int k = 0; k < MW; ++k) pm[8 + k] = m[k];
+    uint32_t rh[16];
+    sha512_oneblock_le32<8 + MW>(rh, pm);
+    uint32_t r[8];
+    sc_reduce512(r, rh);
+    uint32_t Rw[8];
+    ge_compress_w(Rw, comb_sB_minus_hA<false>(r, zero8, btab, nullptr));
+    uint32_t ram[16 + MW];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        ram[k] = Rw[k];
+        ram[8 + k] = Aw[k];
+    }
+#pragma unroll
+    for (int k = 0; k < MW; ++k) ram[16 + k] = m[k];
+    uint32_t kh[16];
+    sha512_oneblock_le32<16 + MW>(kh, ram);
+    uint32_t kk[8];
+    sc_reduce512(kk, kh);
+    uint32_t s[8];
+    sc_muladd(s, kk, a, r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        pk[k] = Aw[k];
+        sig[k] = Rw[k];
+        sig[8 + k] = s[k];
+    }
+}
+
+}  // namespace nw

@@ -1,0 +1,74 @@
+// Kernel parameter blocks and launchers shared by nw_kernels.hip and the C-ABI host layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "../../include/nwcrypto.h"
+
+namespace nw {
+
+// key_info bits (per cached key)
+static constexpr uint32_t KI_OK = 1u;             // decodes (dalek::PublicKey::from_bytes ok)
+static constexpr uint32_t KI_SMALL = 2u;          // small order
+static constexpr uint32_t KI_TORSION_SHIFT = 4;   // 3 bits: t with A^t = t * T8
+static constexpr uint32_t NW_F_TCOEF_SHIFT = 8;   // 3 bits of per-signature torsion coefficient
+static constexpr int SLOW_WORDS = 48;             // slow-path record: point (40 words) + z (4) + pad
+
+struct VerifyParams {
+    uint32_t n;                    // signatures
+    uint32_t batch_mode;           // 0: strict flags only; 1: batch bookkeeping (z, slow list)
+    const uint8_t* sig;            // [n][64]  R || S
+    const uint32_t* signer;        // [n] key-cache slot
+    const uint32_t* sig_cert;      // [n] certificate / batch index (local)
+    const uint32_t* cert_first;    // [ncerts] first signature of each certificate
+    const uint8_t* cert_msg;       // MSGMODE 0: [ncerts][32]
+    const uint8_t* msg_base;       // MSGMODE 1: packed messages
+    const uint64_t* msg_off;       // MSGMODE 1: [n]
+    const uint64_t* msg_len;       // MSGMODE 1: [n]
+    uint64_t cert_base;            // global index of certificate 0 (z stream nonce)
+    const uint32_t* keys_raw;      // [K][8] raw key words (as hashed)
+    const uint32_t* key_info;      // [K]
+    const uint32_t* key_tab;       // [K][COMB_WORDS]
+    const uint32_t* btab;          // [COMB_WORDS] basepoint comb
+    uint32_t zseed[8];
+    uint32_t* flags;               // [n] NW_F_* bits
+    uint32_t* slow_count;          // [1]
+    uint32_t* slow_list;           // [n]
+    uint32_t* slow_slot;           // [n]
+    uint32_t* slow_buf;            // [n][SLOW_WORDS]
+};
+
+struct SlowParams {
+    const uint32_t* slow_count;
+    const uint32_t* slow_list;
+    uint32_t* slow_buf;
+    const uint8_t* sig;
+    uint32_t* flags;
+};
+
+struct FinalizeParams {
+    uint32_t ncerts;
+    const uint32_t* cert_first;
+    const uint32_t* cert_n;
+    const uint32_t* flags;
+    const uint32_t* signer;
+    const uint32_t* stake;         // [K]
+    const uint32_t* slow_slot;
+    const uint32_t* slow_buf;
+    uint8_t* cert_ok;              // [ncerts] (may be null)
+    uint64_t* accepted_stake;      // [ncerts] (may be null)
+};
+
+hipError_t launch_verify(const VerifyParams& p, int msgmode, hipStream_t st);
+hipError_t launch_slow(const SlowParams& p, uint32_t n_upper, hipStream_t st);
+hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st);
+hipError_t launch_expand_certs(uint32_t ncerts, const uint32_t* first, const uint32_t* nv, uint32_t* sig_cert,
+                               hipStream_t st);
+hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hipStream_t st);
+hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
+                           uint32_t* tab, hipStream_t st);
+hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                              uint8_t* out, hipStream_t st);
+hipError_t launch_sign(uint32_t n, int msg_words, const uint32_t* seeds, const uint32_t* msgs,
+                       const uint32_t* btab, uint32_t* pk, uint32_t* sig, hipStream_t st);
+
+}  // namespace nw

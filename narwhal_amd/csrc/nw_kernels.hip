@@ -1,0 +1,367 @@
+// gfx950 kernels for the Ed25519 verify + SHA-512 hot path.
+//
+// Verification strategy: for signature i with committee key A_i,
+//     P_i = s_i B - h_i A_i          (two fixed-base combs, 64 mixed additions, no doublings)
+// is compared with the signature's R encoding after ONE wave-batched inversion.  P_i == R_i is
+// exactly dalek's strict equation (verify_strict).  The cofactorless batch equation of
+// dalek::verify_batch with coefficients z_i,
+//     sum_i [ z_i R_i + (z_i h_i mod l) A_i ] - (sum_i z_i s_i mod l) B == O,
+// decomposes exactly (with D_i = R_i - P_i, A_i^t the 8-torsion part of A_i, l = 5 mod 8) into
+//     sum_i z_i D_i  +  sum_i ((r_i - z_i h_i) mod 8) A_i^t == O,      r_i = z_i h_i mod l,
+// so a certificate whose signatures all satisfy D_i = O and whose keys are torsion-free is accepted
+// without any variable-base work; everything else goes to the exact path (k_slow_sig), which
+// evaluates the remaining terms literally.  Verdicts are therefore identical to dalek's for every
+// input (not just honest ones) given the same z_i.
+#include <hip/hip_runtime.h>
+#include "nw_point.h"
+#include "nw_sha512.h"
+#include "nw_chacha.h"
+#include "nw_kernels.h"
+#include "nw_core.h"
+
+namespace nw {
+
+// ------------------------------------------------------------------------------------ wave helpers
+__device__ __forceinline__ fe shfl_fe(const fe& a, int src) {
+    fe r;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) r.v[k] = (uint32_t)__shfl((int)a.v[k], src, 64);
+    return r;
+}
+
+__device__ __forceinline__ fe shfl_up_fe(const fe& a, unsigned d) {
+    fe r;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) r.v[k] = (uint32_t)__shfl_up((int)a.v[k], d, 64);
+    return r;
+}
+
+__device__ __forceinline__ fe shfl_down_fe(const fe& a, unsigned d) {
+    fe r;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) r.v[k] = (uint32_t)__shfl_down((int)a.v[k], d, 64);
+    return r;
+}
+
+// Montgomery's trick across the 64 lanes of a wave: every lane gets 1/z_lane for the cost of
+// one inversion per wave plus two log-depth product scans.  All 64 lanes must call it.
+__device__ fe wave_batch_invert(const fe& z) {
+    const int lane = threadIdx.x & 63;
+    const fe one = fe_one();
+    fe pre = z;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        fe t = shfl_up_fe(pre, off);
+        t = fe_select(t, one, lane < off);
+        pre = fe_mul(pre, t);
+    }
+    fe suf = z;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        fe t = shfl_down_fe(suf, off);
+        t = fe_select(t, one, lane + off >= 64);
+        suf = fe_mul(suf, t);
+    }
+    const fe inv_all = fe_invert(shfl_fe(pre, 63));
+    fe pre_ex = shfl_up_fe(pre, 1);
+    pre_ex = fe_select(pre_ex, one, lane == 0);
+    fe suf_ex = shfl_down_fe(suf, 1);
+    suf_ex = fe_select(suf_ex, one, lane == 63);
+    return fe_mul(fe_mul(inv_all, pre_ex), suf_ex);
+}
+
+// ------------------------------------------------------------------------------------ verify
+template <int MSGMODE>
+__global__ void __launch_bounds__(256) k_verify(VerifyParams a) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = gid < a.n;
+    const uint32_t i = live ? gid : a.n - 1;
+
+    uint32_t R[8], S[8], Aw[8];
+    load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
+    load_w8(S, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16 + 8);
+    const uint32_t slot = a.signer[i];
+    load_w8(Aw, a.keys_raw + (size_t)slot * 8);
+    const uint32_t kinfo = a.key_info[slot];
+    const uint32_t cert = a.sig_cert[i];
+
+    const bool sok = sc_is_canonical(S);
+    const bool aok = (kinfo & KI_OK) != 0;
+
+    uint32_t h[8];
+    if (MSGMODE == 0) {
+        uint32_t M[8];
+        load_w8(M, reinterpret_cast<const uint32_t*>(a.cert_msg) + (size_t)cert * 8);
+        hram_msg32(h, R, Aw, M);
+    } else {
+        uint32_t hw[16];
+        hram_generic(hw, R, Aw, a.msg_base + a.msg_off[i], a.msg_len[i]);
+        sc_reduce512(h, hw);
+    }
+
+    const ge_p3 P = compute_P(S, h, sok, a.btab, a.key_tab + (size_t)slot * COMB_WORDS);
+
+    // affine P via one inversion per wave
+    const fe zi = wave_batch_invert(live ? P.Z : fe_one());
+    uint32_t flags = match_flags(P, zi, R, sok, aok, (kinfo & KI_SMALL) != 0);
+    const bool match = (flags & NW_F_MATCH) != 0;
+
+    if (a.batch_mode && live) {
+        const uint32_t tk = (kinfo >> KI_TORSION_SHIFT) & 7u;
+        const bool need_z = sok && aok && (!match || tk != 0);
+        if (need_z) {
+            uint32_t z4[4];
+            const uint64_t bidx = a.cert_base + cert;
+            chacha20_z(z4, a.zseed, i - a.cert_first[cert], (uint32_t)bidx, (uint32_t)(bidx >> 32), 0u);
+            if (tk != 0) flags |= torsion_coef(z4, h, tk) << NW_F_TCOEF_SHIFT;
+            if (!match) {
+                flags |= NW_F_SLOW;
+                const uint32_t slot_out = atomicAdd(a.slow_count, 1u);
+                a.slow_list[slot_out] = i;
+                a.slow_slot[i] = slot_out;
+                uint32_t* dst = a.slow_buf + (size_t)slot_out * SLOW_WORDS;
+                store_p3(dst, P);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) dst[40 + k] = z4[k];
+            }
+        }
+    }
+    if (live) a.flags[i] = flags;
+}
+
+// Exact path for signatures with D_i != O: Q_i = z_i (R_i - P_i); R decode failure -> F_R_BAD.
+__global__ void __launch_bounds__(256) k_slow_sig(SlowParams a) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= *a.slow_count) return;
+    const uint32_t i = a.slow_list[t];
+    uint32_t* buf = a.slow_buf + (size_t)t * SLOW_WORDS;
+    uint32_t R[8];
+    load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
+    ge_p3 Rp;
+    const bool rok = ge_decompress(Rp, R);
+    if (!rok) {
+        a.flags[i] |= NW_F_R_BAD;
+        store_p3(buf, ge_identity());
+        return;
+    }
+    uint32_t z[4] = {buf[40], buf[41], buf[42], buf[43]};
+    store_p3(buf, slow_term(Rp, load_p3(buf), z));
+}
+
+// Per-certificate verdict: definitive Err on any bad S / undecodable A / undecodable R, else the
+// exact remaining batch sum (usually empty) must be the identity.
+__global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= a.ncerts) return;
+    const uint32_t first = a.cert_first[c], nv = a.cert_n[c];
+    bool bad = false, slow = false;
+    uint32_t tsum = 0;
+    uint64_t stake = 0;
+    for (uint32_t v = 0; v < nv; ++v) {
+        const uint32_t f = a.flags[first + v];
+        bad = bad || ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) || (f & NW_F_R_BAD);
+        slow = slow || (f & NW_F_SLOW);
+        tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
+        if (f & NW_F_STRICT) stake += a.stake[a.signer[first + v]];
+    }
+    bool ok;
+    if (bad) {
+        ok = false;
+    } else if (!slow) {
+        ok = (tsum & 7u) == 0;
+    } else {
+        ge_p3 acc = ge_identity();
+        for (uint32_t v = 0; v < nv; ++v) {
+            const uint32_t f = a.flags[first + v];
+            if (f & NW_F_SLOW) {
+                const ge_p3 Q = load_p3(a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS);
+                acc = ge_add(acc, ge_to_cached(Q));
+            }
+        }
+        const ge_cached t8c = ge_to_cached(ge_t8());
+        for (uint32_t k = 0; k < (tsum & 7u); ++k) acc = ge_add(acc, t8c);
+        ok = ge_is_identity(acc);
+    }
+    if (a.cert_ok) a.cert_ok[c] = ok ? 1 : 0;
+    if (a.accepted_stake) a.accepted_stake[c] = stake;
+}
+
+__global__ void __launch_bounds__(256) k_expand_certs(uint32_t ncerts, const uint32_t* cert_first,
+                                                      const uint32_t* cert_n, uint32_t* sig_cert) {
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncerts) return;
+    const uint32_t f = cert_first[c], n = cert_n[c];
+    for (uint32_t v = 0; v < n; ++v) sig_cert[f + v] = c;
+}
+
+__global__ void __launch_bounds__(256) k_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) ok[i] = (flags[i] & NW_F_STRICT) ? 1 : 0;
+}
+
+// ------------------------------------------------------------------------------------ key cache
+// One thread per key: decode, small-order flag, torsion index, comb bases 256^i A.
+__global__ void __launch_bounds__(64) k_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info,
+                                                 uint32_t* bases) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nk) return;
+    key_info[j] = key_prep_one(keys_raw + (size_t)j * 8, bases + (size_t)j * COMB_POS * 40);
+}
+
+// One thread per (key, position, entry): entry e of position pos = e * 256^pos * A, affine Niels.
+__global__ void __launch_bounds__(256) k_comb_entries(uint32_t nk, const uint32_t* bases, uint32_t* tab) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t per_key = (uint64_t)COMB_POS * COMB_ENT;
+    if (gid >= (uint64_t)nk * per_key) return;
+    const uint32_t j = (uint32_t)(gid / per_key);
+    const uint32_t rem = (uint32_t)(gid % per_key);
+    comb_entry_one(bases + (size_t)j * COMB_POS * 40, rem / COMB_ENT, rem % COMB_ENT,
+                   tab + (size_t)j * COMB_WORDS);
+}
+
+// ------------------------------------------------------------------------------------ SHA-512 bulk
+// One lane per message (each message is an inherently sequential compression chain).
+__global__ void __launch_bounds__(256) k_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off,
+                                                     const uint64_t* len, uint8_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* m = base + off[i];
+    const uint64_t L = len[i];
+    const uint64_t nfull = L / 128;
+    uint64_t st[8];
+    sha512_init(st);
+    uint64_t w[16];
+    const bool aligned = (reinterpret_cast<uintptr_t>(m) & 3u) == 0;
+    for (uint64_t b = 0; b < nfull; ++b) {
+        const uint8_t* blk = m + b * 128;
+        if (aligned) {
+            const uint32_t* p = reinterpret_cast<const uint32_t*>(blk);
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[k] = be64_from_le32(p[2 * k], p[2 * k + 1]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                uint64_t x = 0;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x = (x << 8) | blk[8 * k + j];
+                w[k] = x;
+            }
+        }
+        sha512_compress(st, w);
+    }
+    // tail: remaining bytes + padding (1 or 2 blocks)
+    const uint64_t rem = L - nfull * 128;
+    const uint8_t* tail = m + nfull * 128;
+    const int tb = rem + 17 <= 128 ? 1 : 2;
+    for (int b = 0; b < tb; ++b) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            uint64_t x = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint64_t p = (uint64_t)b * 128 + 8 * k + j;
+                const uint32_t byte = p < rem ? tail[p] : (p == rem ? 0x80u : 0u);
+                x = (x << 8) | byte;
+            }
+            w[k] = x;
+        }
+        if (b == tb - 1) {
+            w[14] = L >> 61;
+            w[15] = L << 3;
+        }
+        sha512_compress(st, w);
+    }
+    uint32_t d[16];
+    sha512_digest_le32(d, st);
+    uint4* o = reinterpret_cast<uint4*>(out + (size_t)i * 64);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
+}
+
+// ------------------------------------------------------------------------------------ signing
+template <int MW>
+__global__ void __launch_bounds__(256) k_sign(uint32_t n, const uint32_t* seeds, const uint32_t* msgs,
+                                              const uint32_t* btab, uint32_t* pk_out, uint32_t* sig_out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint32_t pk[8], sig[16];
+    sign_one<MW>(seeds + (size_t)i * 8, msgs + (size_t)i * MW, btab, pk, sig);
+    if (pk_out) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) pk_out[(size_t)i * 8 + k] = pk[k];
+    }
+    if (sig_out) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sig_out[(size_t)i * 16 + k] = sig[k];
+    }
+}
+
+// ------------------------------------------------------------------------------------ launchers
+static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
+hipError_t launch_verify(const VerifyParams& p, int msgmode, hipStream_t st) {
+    if (p.n == 0) return hipSuccess;
+    if (msgmode == 0)
+        hipLaunchKernelGGL(k_verify<0>, dim3(blocks_for(p.n, 256)), dim3(256), 0, st, p);
+    else
+        hipLaunchKernelGGL(k_verify<1>, dim3(blocks_for(p.n, 256)), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_slow(const SlowParams& p, uint32_t n_upper, hipStream_t st) {
+    if (n_upper == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_slow_sig, dim3(blocks_for(n_upper, 256)), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
+    if (p.ncerts == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cert_finalize, dim3(blocks_for(p.ncerts, 256)), dim3(256), 0, st, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_expand_certs(uint32_t ncerts, const uint32_t* first, const uint32_t* nv, uint32_t* sig_cert,
+                               hipStream_t st) {
+    if (ncerts == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_expand_certs, dim3(blocks_for(ncerts, 256)), dim3(256), 0, st, ncerts, first, nv,
+                       sig_cert);
+    return hipGetLastError();
+}
+
+hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_flags_to_ok, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, flags, ok);
+    return hipGetLastError();
+}
+
+hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
+                           uint32_t* tab, hipStream_t st) {
+    if (nk == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_key_prep, dim3(blocks_for(nk, 64)), dim3(64), 0, st, nk, keys_raw, key_info, bases);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const uint64_t total = (uint64_t)nk * COMB_POS * COMB_ENT;
+    hipLaunchKernelGGL(k_comb_entries, dim3(blocks_for(total, 256)), dim3(256), 0, st, nk, bases, tab);
+    return hipGetLastError();
+}
+
+hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                              uint8_t* out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sha512_many, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, base, off, len, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_sign(uint32_t n, int msg_words, const uint32_t* seeds, const uint32_t* msgs,
+                       const uint32_t* btab, uint32_t* pk, uint32_t* sig, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    if (msg_words == 8)
+        hipLaunchKernelGGL(k_sign<8>, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, seeds, msgs, btab, pk, sig);
+    else if (msg_words == 2)
+        hipLaunchKernelGGL(k_sign<2>, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, seeds, msgs, btab, pk, sig);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+}  // namespace nw

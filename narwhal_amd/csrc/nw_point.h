@@ -1,0 +1,259 @@
+// edwards25519 group arithmetic for gfx950 (twisted Edwards, a = -1).
+//
+//   ge_p3      extended (X:Y:Z:T), x = X/Z, y = Y/Z, xy = T/Z
+//   ge_precomp affine Niels (y+x, y-x, 2dxy): fixed-base table entries, 7M mixed addition
+//   ge_cached  projective Niels (Y+X, Y-X, Z, 2dT): variable-base operands, 8M addition
+//
+// All formulas are the complete unified ones (Hisil-Wong-Carter-Dawson 2008), so results are the
+// exact group elements curve25519-dalek computes for any decodable input, torsion included.
+#pragma once
+#include "nw_field.h"
+#include "nw_scalar.h"
+
+namespace nw {
+
+struct ge_p3 {
+    fe X, Y, Z, T;
+};
+struct ge_precomp {
+    fe ypx, ymx, xy2d;
+};
+struct ge_cached {
+    fe YpX, YmX, Z, T2d;
+};
+
+// Table entry layout in HBM: 32 u32 words = 128 B (one cache line):
+//   [0..9] y+x, [10..19] y-x, [20..29] 2dxy, [30..31] zero pad.
+static constexpr int PRECOMP_WORDS = 32;
+// Fixed-base comb: 32 positions of signed radix-2^8 digits, entries |d| = 0..128 (0 = identity).
+static constexpr int COMB_POS = 32;
+static constexpr int COMB_ENT = 129;
+static constexpr int COMB_WORDS = COMB_POS * COMB_ENT * PRECOMP_WORDS;   // per point (528,384 B)
+
+NW_HD ge_p3 ge_identity() {
+    ge_p3 r;
+    r.X = fe_zero();
+    r.Y = fe_one();
+    r.Z = fe_one();
+    r.T = fe_zero();
+    return r;
+}
+
+NW_HD ge_precomp ge_precomp_identity() {
+    ge_precomp r;
+    r.ypx = fe_one();
+    r.ymx = fe_one();
+    r.xy2d = fe_zero();
+    return r;
+}
+
+// p + q (mixed).  Limb budget: (Y1+X1) k=2, D = 2Z1 k=2, G = D + C k=3, xy2d may be k=2 (negated).
+NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) {
+    const fe a = fe_mul(fe_sub(p.Y, p.X), q.ymx);
+    const fe b = fe_mul(fe_add(p.Y, p.X), q.ypx);
+    const fe c = fe_mul(p.T, q.xy2d);
+    const fe d = fe_add(p.Z, p.Z);
+    const fe e = fe_sub(b, a);
+    const fe h = fe_add(b, a);
+    const fe f = fe_sub(d, c);
+    const fe g = fe_add(d, c);
+    ge_p3 r;
+    r.X = fe_mul(e, f);
+    r.Y = fe_mul(g, h);
+    r.Z = fe_mul(g, f);
+    r.T = fe_mul(e, h);
+    return r;
+}
+
+NW_HD ge_cached ge_to_cached(const ge_p3& p) {
+    ge_cached c;
+    c.YpX = fe_carry(fe_add(p.Y, p.X));
+    c.YmX = fe_sub(p.Y, p.X);
+    c.Z = p.Z;
+    c.T2d = fe_mul(p.T, fe_from_const(FE_D2));
+    return c;
+}
+
+NW_HD ge_cached ge_cached_neg(const ge_cached& q) {
+    ge_cached r;
+    r.YpX = q.YmX;
+    r.YmX = q.YpX;
+    r.Z = q.Z;
+    r.T2d = fe_carry(fe_neg(q.T2d));
+    return r;
+}
+
+// p + q (both projective)
+NW_HD ge_p3 ge_add(const ge_p3& p, const ge_cached& q) {
+    const fe a = fe_mul(fe_sub(p.Y, p.X), q.YmX);
+    const fe b = fe_mul(fe_add(p.Y, p.X), q.YpX);
+    const fe c = fe_mul(p.T, q.T2d);
+    const fe zz = fe_mul(p.Z, q.Z);
+    const fe d = fe_add(zz, zz);
+    const fe e = fe_sub(b, a);
+    const fe h = fe_add(b, a);
+    const fe f = fe_sub(d, c);
+    const fe g = fe_add(d, c);
+    ge_p3 r;
+    r.X = fe_mul(e, f);
+    r.Y = fe_mul(g, h);
+    r.Z = fe_mul(g, f);
+    r.T = fe_mul(e, h);
+    return r;
+}
+
+// 2p (dbl-2008-hwcd, a = -1)
+NW_HD ge_p3 ge_dbl(const ge_p3& p) {
+    const fe xx = fe_sq(p.X);
+    const fe yy = fe_sq(p.Y);
+    const fe zz = fe_sq(p.Z);
+    const fe zz2 = fe_add(zz, zz);
+    const fe s = fe_sq(fe_add(p.X, p.Y));
+    const fe yr = fe_add(yy, xx);        // k=2
+    const fe zr = fe_sub(yy, xx);        // tight
+    const fe xr = fe_sub(s, yr);         // tight
+    const fe tr = fe_sub(zz2, zr);       // tight
+    ge_p3 r;
+    r.X = fe_mul(xr, tr);
+    r.Y = fe_mul(yr, zr);
+    r.Z = fe_mul(zr, tr);
+    r.T = fe_mul(xr, yr);
+    return r;
+}
+
+NW_HD ge_p3 ge_neg(const ge_p3& p) {
+    ge_p3 r = p;
+    r.X = fe_carry(fe_neg(p.X));
+    r.T = fe_carry(fe_neg(p.T));
+    return r;
+}
+
+NW_HD ge_p3 ge_select(const ge_p3& a, const ge_p3& b, bool take_b) {
+    ge_p3 r;
+    r.X = fe_select(a.X, b.X, take_b);
+    r.Y = fe_select(a.Y, b.Y, take_b);
+    r.Z = fe_select(a.Z, b.Z, take_b);
+    r.T = fe_select(a.T, b.T, take_b);
+    return r;
+}
+
+// EdwardsPoint::is_identity (projective): X == 0 and Y == Z.
+NW_HD bool ge_is_identity(const ge_p3& p) {
+    return fe_iszero(p.X) && fe_eq(p.Y, p.Z);
+}
+
+// Projective equality (EdwardsPoint::ct_eq): X1 Z2 == X2 Z1 and Y1 Z2 == Y2 Z1.
+NW_HD bool ge_eq(const ge_p3& p, const ge_p3& q) {
+    return fe_eq(fe_mul(p.X, q.Z), fe_mul(q.X, p.Z)) && fe_eq(fe_mul(p.Y, q.Z), fe_mul(q.Y, p.Z));
+}
+
+// curve25519-dalek CompressedEdwardsY::decompress (oracle/ed25519_oracle.py decompress):
+// y taken mod p without rejecting y >= p; sqrt_ratio_i failure -> false; x negated when the
+// sign bit is set (x = 0 with the sign bit set is accepted).
+NW_HD bool ge_decompress(ge_p3& out, const uint32_t w[8]) {
+    const fe y = fe_frombytes_w(w);
+    const fe yy = fe_sq(y);
+    const fe u = fe_sub(yy, fe_one());
+    const fe v = fe_add(fe_mul(yy, fe_from_const(FE_D)), fe_one());
+    fe x;
+    const bool ok = fe_sqrt_ratio_i(x, u, v);
+    const bool sign = (w[7] >> 31) != 0;
+    x = fe_select(x, fe_carry(fe_neg(x)), sign);
+    out.X = x;
+    out.Y = fe_carry(y);
+    out.Z = fe_one();
+    out.T = fe_mul(x, y);
+    return ok;
+}
+
+// Canonical compressed encoding (8 LE words): y with the sign of x in bit 255.
+NW_HD void ge_compress_w(uint32_t out[8], const ge_p3& p) {
+    const fe zi = fe_invert(p.Z);
+    uint32_t xw[8];
+    fe_tobytes_w(xw, fe_mul(p.X, zi));
+    fe_tobytes_w(out, fe_mul(p.Y, zi));
+    out[7] |= (xw[0] & 1u) << 31;
+}
+
+NW_HD bool words_eq8(const uint32_t a[8], const uint32_t b[8]) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) d |= a[i] ^ b[i];
+    return d == 0;
+}
+
+// A point with canonical affine y = yw is of small order (order | 8) iff y is one of the five
+// y-coordinates of E[8]: 0, 1, -1, +-y8.
+NW_HD bool y_is_small_order(const uint32_t yw[8]) {
+    return words_eq8(yw, Y_SMALL_0) || words_eq8(yw, Y_SMALL_1) || words_eq8(yw, Y_SMALL_M1) ||
+           words_eq8(yw, Y_SMALL_8) || words_eq8(yw, Y_SMALL_M8);
+}
+
+// Conditionally negate an affine Niels entry: -(x, y) = (-x, y) swaps y+x / y-x and negates 2dxy.
+NW_HD ge_precomp ge_precomp_cneg(const ge_precomp& q, bool neg) {
+    ge_precomp r;
+    r.ypx = fe_select(q.ypx, q.ymx, neg);
+    r.ymx = fe_select(q.ymx, q.ypx, neg);
+    r.xy2d = fe_select(q.xy2d, fe_neg(q.xy2d), neg);   // k <= 2
+    return r;
+}
+
+NW_HD ge_precomp ge_precomp_from_words(const uint32_t* w) {
+    ge_precomp q;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        q.ypx.v[i] = w[i];
+        q.ymx.v[i] = w[10 + i];
+        q.xy2d.v[i] = w[20 + i];
+    }
+    return q;
+}
+
+// Affine Niels form of p (one inversion); tight limbs.
+NW_HD ge_precomp ge_to_precomp(const ge_p3& p) {
+    const fe zi = fe_invert(p.Z);
+    const fe x = fe_mul(p.X, zi);
+    const fe y = fe_mul(p.Y, zi);
+    ge_precomp q;
+    q.ypx = fe_carry(fe_add(y, x));
+    q.ymx = fe_sub(y, x);
+    q.xy2d = fe_mul(fe_mul(x, y), fe_from_const(FE_D2));
+    return q;
+}
+
+// Signed radix-2^8 recoding, consumed one digit per call: s holds the remaining scalar bits
+// (8 LE words, value < 2^253 so the top digit needs no carry-out).  Returns d in [-128, 128].
+NW_HD int next_digit256(uint32_t s[8], int& carry) {
+    const int b = (int)(s[0] & 0xFFu) + carry;
+    carry = (b + 128) >> 8;
+    const int d = b - (carry << 8);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) s[k] = (s[k] >> 8) | (s[k + 1] << 24);
+    s[7] >>= 8;
+    return d;
+}
+
+// Variable-base k*P for a scalar of NW 32-bit LE words, binary method with a uniform add per bit
+// (used only on the rare exact-batch path and at committee load).  The scalar is consumed by
+// shifting, so no runtime-indexed array is needed.
+template <int NW>
+NW_HD ge_p3 ge_scalarmult_vartime(const uint32_t* kin, const ge_p3& p) {
+    uint32_t k[NW];
+#pragma unroll
+    for (int i = 0; i < NW; ++i) k[i] = kin[i];
+    const ge_cached pc = ge_to_cached(p);
+    ge_p3 acc = ge_identity();
+#pragma nounroll
+    for (int i = 0; i < 32 * NW; ++i) {
+        acc = ge_dbl(acc);
+        const bool bit = (k[NW - 1] >> 31) != 0;
+#pragma unroll
+        for (int j = NW - 1; j > 0; --j) k[j] = (k[j] << 1) | (k[j - 1] >> 31);
+        k[0] <<= 1;
+        const ge_p3 t = ge_add(acc, pc);
+        acc = ge_select(acc, t, bit);
+    }
+    return acc;
+}
+
+}  // namespace nw

@@ -421,3 +421,12 @@ def small_order_points() -> List[tuple]:
         if len(pts) == 8:
             break
     return pts
+
+
+def small_order_generator() -> tuple:
+    """The generator T8 of E[8] used by the device code (tools/gen_constants.py): the first point
+    of ``small_order_points()`` of exact order 8."""
+    for q in small_order_points():
+        if not pt_is_identity(pt_mul(4, q)):
+            return q
+    raise AssertionError("no order-8 point")
