@@ -128,6 +128,12 @@ int nw_sign_many(nw_ctx* ctx, const uint8_t (*seed)[32], const uint8_t* msgs, si
 int nw_sign_many_dev(nw_ctx* ctx, const uint8_t* d_seed32, const uint8_t* d_msgs, size_t msg_len,
                      size_t n, uint8_t* d_pk32, uint8_t* d_sig64, void* stream);
 
+/* ---- measurement --------------------------------------------------------------------------
+ * When enabled, HIP events are recorded on the launch stream around every k_verify launch; read
+ * back (synchronizing those events) the summed device time and launch count, then reset. */
+int nw_profile_enable(nw_ctx* ctx, int on);
+int nw_profile_read(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launches);
+
 /* Library build identifier (gfx target, build date). */
 const char* nw_version(void);
 

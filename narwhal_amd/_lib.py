@@ -1,0 +1,281 @@
+"""ctypes binding of libnwcrypto.so (include/nwcrypto.h).
+
+The shared library is built in-tree (``narwhal_amd/libnwcrypto.so``, see ``__graft_entry__.build``).
+There is deliberately no CPU fallback: a missing library raises ``ImportError`` here, and a
+missing/unusable GPU makes every context creation fail with ``DeviceError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnwcrypto.so")
+
+NW_OK, NW_ERR_SIG, NW_ERR_ARG, NW_ERR_DEVICE, NW_ERR_NOMEM = 0, 1, 2, 3, 4
+F_S_OK, F_A_OK, F_MATCH, F_STRICT, F_A_SMALL, F_R_SMALL = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20
+F_SLOW, F_R_BAD = 0x1000, 0x2000
+
+
+class DeviceError(RuntimeError):
+    """The GPU path is unavailable or failed (NW_ERR_DEVICE / NW_ERR_NOMEM / NW_ERR_ARG)."""
+
+
+class NwOpts(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("flags", ctypes.c_uint32), ("max_keys", ctypes.c_size_t)]
+
+
+class NwCert(ctypes.Structure):
+    _fields_ = [("first_vote", ctypes.c_uint32), ("n_votes", ctypes.c_uint32)]
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            "libnwcrypto.so not built (%s); run `python -c 'import __graft_entry__ as g; g.build()'`" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    P, S, U32, U64, I = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    sig = {
+        "nw_ctx_create": (I, [ctypes.POINTER(P), ctypes.POINTER(NwOpts)]),
+        "nw_ctx_destroy": (None, [P]),
+        "nw_last_error": (ctypes.c_char_p, [P]),
+        "nw_committee_load": (I, [P, P, P, S, P]),
+        "nw_committee_size": (S, [P]),
+        "nw_verify_strict": (I, [P, P, S, P, P]),
+        "nw_verify_strict_many": (I, [P, P, P, P, P, S, P]),
+        "nw_verify_batch": (I, [P, P, P, P, P, S, P, U64]),
+        "nw_verify_certs": (I, [P, P, S, P, P, P, P, U64, P, P, P]),
+        "nw_verify_certs_dev": (I, [P, S, P, P, S, P, P, P, P, U64, P, P, P, P]),
+        "nw_sha512": (I, [P, P, S, P]),
+        "nw_sha512_many": (I, [P, P, P, P, S, P]),
+        "nw_sha512_many_dev": (I, [P, P, P, P, S, P, P]),
+        "nw_sign_many": (I, [P, P, P, S, S, P, P]),
+        "nw_sign_many_dev": (I, [P, P, P, S, S, P, P, P]),
+        "nw_profile_enable": (I, [P, I]),
+        "nw_profile_read": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]),
+        "nw_version": (ctypes.c_char_p, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+LIB = _load()
+
+
+def _buf(b: bytes):
+    return ctypes.c_char_p(b) if b else None
+
+
+class Engine:
+    """One nw_ctx (one GPU).  Thread-safe: the C layer serializes calls on a context."""
+
+    def __init__(self, device: int = -1, max_keys: int = 0):
+        self._ctx = ctypes.c_void_p()
+        opts = NwOpts(device, 0, max_keys)
+        rc = LIB.nw_ctx_create(ctypes.byref(self._ctx), ctypes.byref(opts))
+        if rc != NW_OK:
+            raise DeviceError("nw_ctx_create failed (rc=%d): no usable gfx950 GPU" % rc)
+        self.device = device
+
+    # -- plumbing -----------------------------------------------------------------------------
+    @property
+    def handle(self):
+        return self._ctx
+
+    def close(self):
+        if self._ctx:
+            LIB.nw_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc: int, what: str):
+        if rc in (NW_OK, NW_ERR_SIG):
+            return rc
+        err = LIB.nw_last_error(self._ctx)
+        raise DeviceError("%s failed (rc=%d): %s" % (what, rc, err.decode() if err else ""))
+
+    # -- key cache ----------------------------------------------------------------------------
+    def committee_load(self, pks, stakes=None):
+        """Load keys (iterable of 32-byte bytes); returns their slots (list of int)."""
+        pks = [bytes(k) for k in pks]
+        n = len(pks)
+        blob = b"".join(pks)
+        slots = (ctypes.c_uint32 * max(n, 1))()
+        st = None
+        if stakes is not None:
+            st = (ctypes.c_uint32 * n)(*stakes)
+        self.check(LIB.nw_committee_load(self._ctx, _buf(blob), st, n, slots), "nw_committee_load")
+        return list(slots[:n])
+
+    def committee_size(self) -> int:
+        return LIB.nw_committee_size(self._ctx)
+
+    # -- verification -------------------------------------------------------------------------
+    def verify_strict(self, msg: bytes, pk: bytes, sig: bytes) -> bool:
+        rc = self.check(LIB.nw_verify_strict(self._ctx, _buf(msg), len(msg), bytes(pk), bytes(sig)),
+                        "nw_verify_strict")
+        return rc == NW_OK
+
+    def verify_strict_many(self, msgs, pks, sigs):
+        n = len(sigs)
+        if n == 0:
+            return []
+        mp = (ctypes.c_char_p * n)(*[bytes(m) for m in msgs])
+        ln = (ctypes.c_size_t * n)(*[len(m) for m in msgs])
+        ok = (ctypes.c_uint8 * n)()
+        self.check(LIB.nw_verify_strict_many(self._ctx, mp, ln, _buf(b"".join(map(bytes, pks))),
+                                             _buf(b"".join(map(bytes, sigs))), n, ok), "nw_verify_strict_many")
+        return [bool(x) for x in ok]
+
+    def verify_batch(self, msgs, pks, sigs, zseed: bytes, batch_index: int = 0) -> bool:
+        n = len(sigs)
+        if len(msgs) != n or len(pks) != n:
+            return False   # dalek: ArrayLengthError
+        if n == 0:
+            return True
+        mp = (ctypes.c_char_p * n)(*[bytes(m) for m in msgs])
+        ln = (ctypes.c_size_t * n)(*[len(m) for m in msgs])
+        rc = self.check(LIB.nw_verify_batch(self._ctx, mp, ln, _buf(b"".join(map(bytes, pks))),
+                                            _buf(b"".join(map(bytes, sigs))), n, bytes(zseed), batch_index),
+                        "nw_verify_batch")
+        return rc == NW_OK
+
+    def verify_certs(self, cert_ranges, sigs_blob: bytes, signer_slots, msgs_blob: bytes, zseed: bytes,
+                     cert_base: int = 0):
+        """cert_ranges: list of (first_vote, n_votes).  Returns (cert_ok, sig_ok, accepted_stake) lists."""
+        nc = len(cert_ranges)
+        nsig = len(signer_slots)
+        certs = (NwCert * max(nc, 1))(*[NwCert(f, n) for f, n in cert_ranges])
+        slots = (ctypes.c_uint32 * max(nsig, 1))(*signer_slots)
+        cert_ok = (ctypes.c_uint8 * max(nc, 1))()
+        sig_ok = (ctypes.c_uint8 * max(nsig, 1))()
+        stake = (ctypes.c_uint64 * max(nc, 1))()
+        self.check(LIB.nw_verify_certs(self._ctx, certs, nc, _buf(sigs_blob), slots, _buf(msgs_blob), bytes(zseed),
+                                       cert_base, cert_ok, sig_ok, stake), "nw_verify_certs")
+        return [bool(x) for x in cert_ok[:nc]], [bool(x) for x in sig_ok[:nsig]], list(stake[:nc])
+
+    # -- digests ------------------------------------------------------------------------------
+    def sha512(self, data: bytes) -> bytes:
+        out = ctypes.create_string_buffer(64)
+        self.check(LIB.nw_sha512(self._ctx, _buf(data), len(data), out), "nw_sha512")
+        return out.raw
+
+    def sha512_many(self, messages) -> list:
+        n = len(messages)
+        if n == 0:
+            return []
+        offs, lens, pos = [], [], 0
+        for m in messages:
+            offs.append(pos)
+            lens.append(len(m))
+            pos += len(m)
+        blob = b"".join(bytes(m) for m in messages)
+        out = ctypes.create_string_buffer(64 * n)
+        self.check(LIB.nw_sha512_many(self._ctx, _buf(blob) if blob else ctypes.c_char_p(b"\0"),
+                                      (ctypes.c_uint64 * n)(*offs), (ctypes.c_uint64 * n)(*lens), n, out),
+                   "nw_sha512_many")
+        return [out.raw[64 * i:64 * (i + 1)] for i in range(n)]
+
+    # -- signing ------------------------------------------------------------------------------
+    def sign_many(self, seeds, msgs):
+        """RFC 8032 signatures of equal-length (8 or 32 byte) messages; returns (pks, sigs)."""
+        n = len(seeds)
+        if n == 0:
+            return [], []
+        mlen = len(msgs[0])
+        pk = ctypes.create_string_buffer(32 * n)
+        sg = ctypes.create_string_buffer(64 * n)
+        self.check(LIB.nw_sign_many(self._ctx, _buf(b"".join(map(bytes, seeds))), _buf(b"".join(map(bytes, msgs))),
+                                    mlen, n, pk, sg), "nw_sign_many")
+        return ([pk.raw[32 * i:32 * i + 32] for i in range(n)], [sg.raw[64 * i:64 * i + 64] for i in range(n)])
+
+
+    # -- numpy bulk paths (large synthetic workloads) -------------------------------------------
+    def sign_many_np(self, seeds, msgs):
+        """seeds: uint8[N,32]; msgs: uint8[N,L] with L in (8, 32).  Returns (pk uint8[N,32], sig uint8[N,64])."""
+        import numpy as np
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint8)
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        n = seeds.shape[0]
+        pk = np.empty((n, 32), np.uint8)
+        sg = np.empty((n, 64), np.uint8)
+        if n:
+            self.check(LIB.nw_sign_many(self._ctx, seeds.ctypes.data, msgs.ctypes.data, msgs.shape[1], n,
+                                        pk.ctypes.data, sg.ctypes.data), "nw_sign_many")
+        return pk, sg
+
+    def committee_load_np(self, pks, stakes=None):
+        import numpy as np
+        pks = np.ascontiguousarray(pks, dtype=np.uint8)
+        n = pks.shape[0]
+        slots = np.empty(max(n, 1), np.uint32)
+        st = None if stakes is None else np.ascontiguousarray(stakes, dtype=np.uint32)
+        self.check(LIB.nw_committee_load(self._ctx, pks.ctypes.data, None if st is None else st.ctypes.data, n,
+                                         slots.ctypes.data), "nw_committee_load")
+        return slots[:n]
+
+    def verify_certs_np(self, cert_first, cert_n, sigs, signer_slots, msgs, zseed: bytes, cert_base: int = 0):
+        """Host-buffer certificate path (numpy in/out): returns (cert_ok u8[C], sig_ok u8[N], stake u64[C])."""
+        import numpy as np
+        nc = len(cert_first)
+        certs = np.empty((nc, 2), np.uint32)
+        certs[:, 0] = cert_first
+        certs[:, 1] = cert_n
+        sigs = np.ascontiguousarray(sigs, dtype=np.uint8)
+        slots = np.ascontiguousarray(signer_slots, dtype=np.uint32)
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        cert_ok = np.zeros(max(nc, 1), np.uint8)
+        sig_ok = np.zeros(max(len(slots), 1), np.uint8)
+        stake = np.zeros(max(nc, 1), np.uint64)
+        self.check(LIB.nw_verify_certs(self._ctx, certs.ctypes.data, nc, sigs.ctypes.data, slots.ctypes.data,
+                                       msgs.ctypes.data, bytes(zseed), cert_base, cert_ok.ctypes.data,
+                                       sig_ok.ctypes.data, stake.ctypes.data), "nw_verify_certs")
+        return cert_ok[:nc], sig_ok[:len(slots)], stake[:nc]
+
+    def verify_certs_dev(self, ncerts, d_first, d_n, nsigs, d_sig, d_signer, d_msg, zseed: bytes, cert_base,
+                         d_cert_ok, d_flags, d_stake, stream):
+        """Device-pointer path (ints = device addresses, e.g. torch ``data_ptr()``); enqueues only."""
+        self.check(LIB.nw_verify_certs_dev(self._ctx, ncerts, d_first, d_n, nsigs, d_sig, d_signer, d_msg,
+                                           bytes(zseed), cert_base, d_cert_ok, d_flags, d_stake, stream),
+                   "nw_verify_certs_dev")
+
+    def profile_enable(self, on: bool = True):
+        self.check(LIB.nw_profile_enable(self._ctx, 1 if on else 0), "nw_profile_enable")
+
+    def profile_read(self):
+        """(summed k_verify device ms, launches) since the last read; synchronizes the events."""
+        ms = ctypes.c_double(0)
+        n = ctypes.c_uint64(0)
+        self.check(LIB.nw_profile_read(self._ctx, ctypes.byref(ms), ctypes.byref(n)), "nw_profile_read")
+        return ms.value, n.value
+
+    def sha512_many_dev(self, d_base, d_off, d_len, n, d_out, stream):
+        self.check(LIB.nw_sha512_many_dev(self._ctx, d_base, d_off, d_len, n, d_out, stream), "nw_sha512_many_dev")
+
+
+_default: Optional[Engine] = None
+_default_lock = threading.Lock()
+
+
+def default_engine() -> Engine:
+    """Process-wide engine on this process's GPU (LOCAL_RANK, else the current device)."""
+    global _default
+    with _default_lock:
+        if _default is None:
+            dev = int(os.environ.get("LOCAL_RANK", "-1"))
+            _default = Engine(device=dev)
+        return _default
+
+
+def version() -> str:
+    return LIB.nw_version().decode()

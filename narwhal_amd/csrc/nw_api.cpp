@@ -60,6 +60,10 @@ struct nw_ctx {
     uint32_t* d_key_tab = nullptr;
     std::unordered_map<std::string, uint32_t> slot_of;
     std::vector<uint32_t> h_stake;
+    // measurement: (start, stop) event pairs around k_verify launches
+    bool prof_on = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
+    size_t prof_used = 0;
     // workspace
     DevBuf w_bases, w_sig, w_signer, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len,
         w_flags, w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_stake_out, w_ok, w_misc,
@@ -210,6 +214,8 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
     NW_TRY(ctx->w_slow_slot.ensure(nsigs * 4 + 4), "ws slow_slot");
     if (batch_mode) NW_TRY(ctx->w_slow_buf.ensure(nsigs * (size_t)SLOW_WORDS * 4 + 4), "ws slow_buf");
     NW_TRY(hipMemsetAsync(ctx->w_slow_count.p, 0, 16, st), "memset");
+    // votes not covered by any certificate map to certificate 0 (never out of range)
+    NW_TRY(hipMemsetAsync(ctx->w_sig_cert.p, 0, nsigs * 4 + 4, st), "memset sig_cert");
     NW_TRY(launch_expand_certs((uint32_t)ncerts, d_first, d_nv, ctx->w_sig_cert.as<uint32_t>(), st), "k_expand_certs");
 
     VerifyParams vp{};
@@ -234,7 +240,20 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
     vp.slow_list = ctx->w_slow_list.as<uint32_t>();
     vp.slow_slot = ctx->w_slow_slot.as<uint32_t>();
     vp.slow_buf = ctx->w_slow_buf.as<uint32_t>();
+    hipEvent_t ev_stop = nullptr;
+    if (ctx->prof_on && nsigs) {
+        if (ctx->prof_used == ctx->prof_events.size()) {
+            hipEvent_t a, b;
+            NW_TRY(hipEventCreate(&a), "hipEventCreate");
+            NW_TRY(hipEventCreate(&b), "hipEventCreate");
+            ctx->prof_events.emplace_back(a, b);
+        }
+        NW_TRY(hipEventRecord(ctx->prof_events[ctx->prof_used].first, st), "hipEventRecord");
+        ev_stop = ctx->prof_events[ctx->prof_used].second;
+        ++ctx->prof_used;
+    }
     NW_TRY(launch_verify(vp, msgmode, st), "k_verify");
+    if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");
     if (!batch_mode) return NW_OK;
 
     SlowParams sp{};
@@ -381,10 +400,38 @@ void nw_ctx_destroy(nw_ctx* ctx) {
                       &ctx->w_slow_list, &ctx->w_slow_slot, &ctx->w_slow_buf, &ctx->w_cert_ok, &ctx->w_stake_out,
                       &ctx->w_ok, &ctx->w_misc, &ctx->w_out})
         b->release();
+    for (auto& ev : ctx->prof_events) {
+        (void)hipEventDestroy(ev.first);
+        (void)hipEventDestroy(ev.second);
+    }
     for (uint32_t* p : {ctx->d_btab, ctx->d_keys_raw, ctx->d_key_info, ctx->d_stake, ctx->d_key_tab})
         if (p) (void)hipFree(p);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+}
+
+int nw_profile_enable(nw_ctx* ctx, int on) {
+    if (!ctx) return NW_ERR_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    ctx->prof_on = on != 0;
+    return NW_OK;
+}
+
+int nw_profile_read(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launches) {
+    if (!ctx) return NW_ERR_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    double total = 0;
+    for (size_t i = 0; i < ctx->prof_used; ++i) {
+        NW_TRY(hipEventSynchronize(ctx->prof_events[i].second), "hipEventSynchronize");
+        float ms = 0;
+        NW_TRY(hipEventElapsedTime(&ms, ctx->prof_events[i].first, ctx->prof_events[i].second), "elapsed");
+        total += ms;
+    }
+    if (verify_ms_total) *verify_ms_total = total;
+    if (verify_launches) *verify_launches = ctx->prof_used;
+    ctx->prof_used = 0;
+    return NW_OK;
 }
 
 const char* nw_last_error(const nw_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }

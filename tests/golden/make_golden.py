@@ -1,0 +1,193 @@
+"""Generate tests/golden/*.json — run in the build container (not on the GPU box):
+
+    python tests/golden/make_golden.py
+
+Sources (see README.md in this directory):
+* RFC 8032 §7.1 known answers (TEST 1-3 values as published) — checked against the oracle AND
+  libsodium 1.0.18 (/opt/conda/lib/libsodium.so, an independent implementation) when present;
+* the reference's deterministic fixtures, re-derived: keys() = StdRng::from_seed([0;32])
+  (crypto/src/tests/crypto_tests.rs:26-29), the crypto_tests cases (:49-115), the primary
+  header()/votes()/certificate() fixtures (primary/src/tests/common.rs:96-166) and the worker
+  serialized batch digest (worker/src/tests/common.rs:92-109);
+* adversarial vectors (tests/vectors.py) with expected verdicts from the oracle restatement of
+  dalek 1.0.1 — "parity unpinned" w.r.t. the reference, which holds no such vectors.
+"""
+import ctypes
+import json
+import os
+import random
+import struct
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "..", "..", "oracle"))
+sys.path.insert(0, os.path.join(HERE, ".."))
+import ed25519_oracle as o  # noqa: E402
+import vectors  # noqa: E402
+
+SODIUM = "/opt/conda/lib/libsodium.so"
+
+RFC8032 = [
+    # (secret seed, public key, message, signature) — RFC 8032 §7.1 TEST 1, 2, 3
+    ("9d61b19deffd5a60ba844af492ec2cc44449c5697b326919703bac031cae7f60",
+     "d75a980182b10ab7d54bfed3c964073a0ee172f3daa62325af021a68f707511a", "",
+     "e5564300c360ac729086e2cc806e828a84877f1eb8e5d974d873e065224901555fb8821590a33bacc61e39701cf9b46bd25bf5f0595bbe24655141438e7a100b"),
+    ("4ccd089b28ff96da9db6c346ec114e0f5b8a319f35aba624da8cf6ed4fb8a6fb",
+     "3d4017c3e843895a92b70aa74d1b7ebc9c982ccf2ec4968cc0cd55f12af4660c", "72",
+     "92a009a9f0d4cab8720e820b5f642540a2b27b5416503f8fb3762223ebdb69da085ac1e43e15996e458f3613d0f11d8c387b2eaeb4302aeeb00d291612bb0c00"),
+    ("c5aa8df43f9f837bedb7442f31dcb7b166d38535076f094b85ce3a2e0b4458f7",
+     "fc51cd8e6218a1a38da47ed00230f0580816ed13ba3303ac5deb911548908025", "af82",
+     "6291d657deec24024827e69c3abe01a30ce548a284743a445e3680d7db5ac3ac18ff9b538d16f290ae67f760984dc6594a7c15e9716ed28dc027beceea1ec40a"),
+]
+
+
+def sodium():
+    if not os.path.exists(SODIUM):
+        return None
+    lib = ctypes.CDLL(SODIUM)
+    assert lib.sodium_init() >= 0
+    return lib
+
+
+def sodium_sign(lib, seed, msg):
+    pk = ctypes.create_string_buffer(32)
+    sk = ctypes.create_string_buffer(64)
+    assert lib.crypto_sign_seed_keypair(pk, sk, seed) == 0
+    sig = ctypes.create_string_buffer(64)
+    sl = ctypes.c_ulonglong(0)
+    assert lib.crypto_sign_detached(sig, ctypes.byref(sl), msg, ctypes.c_ulonglong(len(msg)), sk) == 0
+    return pk.raw, sig.raw
+
+
+def sodium_verify(lib, pk, msg, sig):
+    return lib.crypto_sign_verify_detached(sig, msg, ctypes.c_ulonglong(len(msg)), pk) == 0
+
+
+def h(b):
+    return b.hex()
+
+
+def main():
+    na = sodium()
+    out = {}
+    # ---------------------------------------------------------------- RFC 8032
+    rfc = []
+    for seed, pk, msg, sig in RFC8032:
+        s, m = bytes.fromhex(seed), bytes.fromhex(msg)
+        assert h(o.public_from_seed(s)) == pk, "oracle pk mismatch vs RFC 8032"
+        assert h(o.sign(s, m)) == sig, "oracle sig mismatch vs RFC 8032"
+        assert o.verify_strict(bytes.fromhex(pk), m, bytes.fromhex(sig))
+        if na:
+            spk, ssig = sodium_sign(na, s, m)
+            assert h(spk) == pk and h(ssig) == sig, "libsodium disagrees with RFC 8032"
+        rfc.append({"seed": seed, "pk": pk, "msg": msg, "sig": sig})
+    out["rfc8032"] = rfc
+
+    # ---------------------------------------------------------------- reference fixtures
+    seeds = o.reference_fixture_seeds(4)
+    keys = [{"seed": h(s), "pk": h(o.public_from_seed(s))} for s in seeds]
+    hello = o.digest32(b"Hello, world!")
+    bad = o.digest32(b"Bad message!")
+    k3 = seeds[3]
+    sig_hello = o.sign(k3, hello)
+    # verify_valid_batch pops keys 3, 2, 1; verify_invalid_batch pops 3, 2 and adds key 1 + default sig
+    valid_batch = [(h(o.public_from_seed(seeds[i])), h(o.sign(seeds[i], hello))) for i in (3, 2, 1)]
+    invalid_batch = valid_batch[:2] + [(h(o.public_from_seed(seeds[1])), "00" * 64)]
+    zseed = bytes(32)
+    assert o.crypto_verify_batch(hello, [(bytes.fromhex(a), bytes.fromhex(b)) for a, b in valid_batch], zseed)
+    assert not o.crypto_verify_batch(hello, [(bytes.fromhex(a), bytes.fromhex(b)) for a, b in invalid_batch], zseed)
+    if na:
+        for s in seeds:
+            assert sodium_sign(na, s, hello)[0] == o.public_from_seed(s)
+        assert sodium_verify(na, o.public_from_seed(k3), hello, sig_hello)
+    out["reference_fixtures"] = {
+        "keys": keys,
+        "hello_digest": h(hello),
+        "bad_digest": h(bad),
+        "verify_valid_signature": {"pk": keys[3]["pk"], "digest": h(hello), "sig": h(sig_hello), "ok": True},
+        "verify_invalid_signature": {"pk": keys[3]["pk"], "digest": h(bad), "sig": h(sig_hello), "ok": False},
+        "verify_valid_batch": {"digest": h(hello), "votes": valid_batch, "ok": True},
+        "verify_invalid_batch": {"digest": h(hello), "votes": invalid_batch, "ok": False},
+    }
+
+    # primary fixtures: header(), votes(header), certificate(header)  (primary/src/tests/common.rs)
+    pks = [o.public_from_seed(s) for s in seeds]
+    genesis_digests = [o.vote_digest(bytes(32), 0, pk) for pk in pks]   # Certificate::digest of genesis
+    author, secret = pks[3], seeds[3]
+    hid = o.header_digest(author, 1, [], genesis_digests)
+    hsig = o.sign(secret, hid)
+    vd = o.vote_digest(hid, 1, author)
+    votes = [(h(pks[i]), h(o.sign(seeds[i], vd))) for i in range(4)]
+    assert o.crypto_verify_batch(vd, [(bytes.fromhex(a), bytes.fromhex(b)) for a, b in votes], zseed)
+    out["primary_fixtures"] = {
+        "header": {"author": h(author), "round": 1, "parents": [h(d) for d in sorted(genesis_digests)],
+                   "id": h(hid), "signature": h(hsig)},
+        "vote_digest": h(vd),
+        "votes": votes,
+        "certificate_digest": h(vd),
+    }
+    batch = o.bincode_worker_batch([bytes(100), bytes(100)])
+    out["worker_batch"] = {"serialized": h(batch), "digest": h(o.digest32(batch)), "len": len(batch)}
+
+    # ---------------------------------------------------------------- SHA-512 lengths
+    rng = random.Random(2024)
+    sha = []
+    for ln in [0, 1, 3, 8, 31, 32, 63, 64, 72, 96, 111, 112, 113, 127, 128, 129, 200, 255, 256, 1000, 4097]:
+        m = bytes(rng.randrange(256) for _ in range(ln))
+        sha.append({"msg": h(m), "sha512": h(o.sha512(m))})
+    out["sha512"] = sha
+
+    # ---------------------------------------------------------------- adversarial strict + batch
+    rng = random.Random(8032)
+    cases = vectors.adversarial_cases(rng)
+    strict = []
+    for name, pk, sig, msg in cases:
+        ok = o.verify_strict(pk, msg, sig)
+        if na and ok:
+            # libsodium is stricter (rejects small order / non-canonical); only honest cases agree
+            pass
+        strict.append({"name": name, "pk": h(pk), "sig": h(sig), "msg": h(msg), "strict": ok})
+    out["adversarial_strict"] = strict
+    honest = vectors.honest_cases(rng, 4)
+    zseed = bytes(range(32))
+    batches = []
+    for idx, (name, pk, sig, msg) in enumerate(cases):
+        items = [(x[1], x[2], x[3]) for x in honest[:3]] + [(pk, sig, msg)]
+        for bidx in (idx, 5000 + idx):
+            want = o.crypto_verify_batch(msg, [(k, s) for k, s, _ in items], zseed, bidx) \
+                if all(m == msg for _, _, m in items) else None
+            zs = o.batch_coefficients(zseed, bidx, len(items))
+            # crypto::verify_batch semantics: S high-bit / key-decode checks first, then dalek
+            pre_ok = all(s[63] & 0xE0 == 0 and o.decompress(k) is not None for k, s, _ in items)
+            want = pre_ok and o.verify_batch_z([m for _, _, m in items], [s for _, s, _ in items],
+                                               [k for k, _, _ in items], zs)
+            batches.append({"name": name, "zseed": h(zseed), "batch_index": bidx,
+                            "items": [[h(k), h(s), h(m)] for k, s, m in items], "ok": want})
+    for bidx in (11, 12):
+        items = vectors.cancelling_pair(zseed, bidx, rng)
+        zs = o.batch_coefficients(zseed, bidx, len(items))
+        want = o.verify_batch_z([m for _, _, m in items], [s for _, s, _ in items], [k for k, _, _ in items], zs)
+        assert want
+        batches.append({"name": "cancelling_pair", "zseed": h(zseed), "batch_index": bidx,
+                        "items": [[h(k), h(s), h(m)] for k, s, m in items], "ok": True})
+        batches.append({"name": "cancelling_pair_other_z", "zseed": h(zseed), "batch_index": bidx + 100,
+                        "items": [[h(k), h(s), h(m)] for k, s, m in items], "ok": False})
+    out["adversarial_batch"] = batches
+
+    # ---------------------------------------------------------------- coefficient stream pin
+    out["nwz_v1"] = [{"zseed": h(zseed), "batch_index": b, "z": [str(z) for z in o.batch_coefficients(zseed, b, 5)]}
+                     for b in (0, 1, 2**33 + 5)]
+    # RFC 8439 §2.3.2 block test vector pins the ChaCha20 block itself
+    key = bytes(range(32))
+    blk = o.chacha20_block(key, 1, bytes.fromhex("000000090000004a00000000"))
+    assert blk.hex().startswith("10f1e7e4d13b5915500fdd1fa32071c4"), "ChaCha20 RFC 8439 vector"
+    out["chacha20_rfc8439"] = {"key": h(key), "counter": 1, "nonce": "000000090000004a00000000", "block": h(blk)}
+
+    path = os.path.join(HERE, "vectors.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print("wrote", path, "sodium cross-check:", bool(na))
+
+
+if __name__ == "__main__":
+    main()
