@@ -128,11 +128,8 @@ def main():
     d_ok = torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev)
     d_flags = torch.zeros(cs.nsigs, dtype=torch.int32, device=dev)
     d_stake = torch.zeros(cs.ncerts, dtype=torch.int64, device=dev)
-    nbits = (cs.ncerts + 7) // 8
-    bit_w = (2 ** torch.arange(8, device=dev, dtype=torch.int32)).to(torch.uint8)
-    pad = nbits * 8 - cs.ncerts
-    gathered_bits = [torch.empty(nbits, dtype=torch.uint8, device=dev) for _ in range(world)]
-    gathered_stake = [torch.empty(cs.ncerts, dtype=torch.int64, device=dev) for _ in range(world)]
+    from narwhal_amd import shard
+    ranges = [(r * args.certs, (r + 1) * args.certs) for r in range(world)]   # node-wide certificate ranges
     zseed = os.urandom(32)
 
     def step():
@@ -141,10 +138,7 @@ def main():
                              d_signer.data_ptr(), d_msg.data_ptr(), zseed, first_cert, d_ok.data_ptr(),
                              d_flags.data_ptr(), d_stake.data_ptr(), stream)
         if world > 1:
-            bits = torch.nn.functional.pad(d_ok, (0, pad)).view(nbits, 8)
-            packed = (bits * bit_w).sum(dim=1, dtype=torch.int32).to(torch.uint8)
-            dist.all_gather(gathered_bits, packed)
-            dist.all_gather(gathered_stake, d_stake)
+            shard.allgather_verdicts(d_ok, d_stake, ranges)   # RCCL all_gather of bitmaps + stake
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,93 @@
+"""Multi-GPU sharding of certificate verification.
+
+Certificates are independent units (``Certificate::verify``, primary/src/messages.rs:189-215), so
+a node's batch is split into contiguous certificate ranges balanced by vote count, one per GPU
+(one process per GPU).  Coefficient streams are keyed by the *global* certificate index
+(NW-Z v1 nonce), so a shard needs nothing from the others to reproduce the single-GPU verdicts.
+The only exchange is the RCCL all-gather of the per-shard verdict bitmaps and stake tallies
+(a few KB: latency-bound, one xGMI hop).
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import numpy as np
+
+
+def partition(cert_n: Sequence[int], world: int) -> List[Tuple[int, int]]:
+    """Contiguous [c0, c1) certificate ranges, one per rank, balanced by total votes."""
+    cert_n = np.asarray(cert_n, dtype=np.int64)
+    nc = cert_n.shape[0]
+    if world <= 1:
+        return [(0, nc)]
+    cum = np.concatenate([[0], np.cumsum(cert_n)])
+    total = int(cum[-1])
+    bounds = [0]
+    for r in range(1, world):
+        target = total * r / world
+        c = int(np.searchsorted(cum, target, side="left"))
+        c = max(bounds[-1], min(c, nc))
+        bounds.append(c)
+    bounds.append(nc)
+    return [(bounds[r], bounds[r + 1]) for r in range(world)]
+
+
+def pack_bits(ok):
+    """uint8 0/1 tensor [n] -> packed little-endian bit tensor [ceil(n/8)] (torch)."""
+    import torch
+    n = ok.shape[0]
+    nb = (n + 7) // 8
+    pad = nb * 8 - n
+    bits = torch.nn.functional.pad(ok.to(torch.uint8), (0, pad)).view(nb, 8).to(torch.int32)
+    w = (2 ** torch.arange(8, device=ok.device, dtype=torch.int32))
+    return (bits * w).sum(dim=1).to(torch.uint8)
+
+
+def unpack_bits(packed, n: int):
+    import torch
+    w = (2 ** torch.arange(8, device=packed.device, dtype=torch.int32))
+    bits = (packed.to(torch.int32).unsqueeze(1) & w) != 0
+    return bits.reshape(-1)[:n].to(torch.uint8)
+
+
+def allgather_verdicts(ok_local, stake_local, ranges: List[Tuple[int, int]], group=None):
+    """All-gather per-shard verdicts (bit-packed) and accepted stake into global [ncerts] tensors.
+
+    ``ok_local``: uint8 [c1 - c0]; ``stake_local``: int64 [c1 - c0] (this rank's range).  Works on
+    any torch.distributed backend (RCCL on GPU tensors, gloo on CPU tensors for tests)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    maxc = max(c1 - c0 for c0, c1 in ranges)
+    maxb = (maxc + 7) // 8
+    dev = ok_local.device
+    bits = torch.zeros(maxb, dtype=torch.uint8, device=dev)
+    pb = pack_bits(ok_local)
+    bits[:pb.shape[0]] = pb
+    stake = torch.zeros(maxc, dtype=torch.int64, device=dev)
+    stake[:stake_local.shape[0]] = stake_local
+    gb = [torch.empty_like(bits) for _ in range(world)]
+    gs = [torch.empty_like(stake) for _ in range(world)]
+    dist.all_gather(gb, bits, group=group)
+    dist.all_gather(gs, stake, group=group)
+    oks, stakes = [], []
+    for r, (c0, c1) in enumerate(ranges):
+        oks.append(unpack_bits(gb[r], c1 - c0))
+        stakes.append(gs[r][:c1 - c0])
+    return torch.cat(oks), torch.cat(stakes)
+
+
+def verify_sharded(engine, cs, slots, zseed: bytes, rank: int, world: int, group=None):
+    """Verify this rank's shard of ``cs`` (narwhal_amd.workload.Certificates) on its GPU and
+    all-gather the node-wide verdicts.  Returns (cert_ok uint8[C], stake int64[C]) torch tensors on
+    this rank's device."""
+    import torch
+    ranges = partition(cs.cert_n, world)
+    c0, c1 = ranges[rank]
+    f0 = int(cs.cert_first[c0]) if c1 > c0 else 0
+    f1 = int(cs.cert_first[c1 - 1] + cs.cert_n[c1 - 1]) if c1 > c0 else 0
+    ok, _, st = engine.verify_certs_np(cs.cert_first[c0:c1] - f0, cs.cert_n[c0:c1], cs.sigs[f0:f1],
+                                       slots[cs.signer[f0:f1]], cs.msgs[c0:c1], zseed, cert_base=c0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    return allgather_verdicts(torch.from_numpy(ok).to(dev), torch.from_numpy(st.astype(np.int64)).to(dev), ranges,
+                              group)
