@@ -46,7 +46,10 @@ typedef struct nw_ctx nw_ctx;
 typedef struct nw_opts {
     int device;        /* HIP device ordinal (one process per GPU; -1 = current device) */
     uint32_t flags;    /* reserved, 0 */
-    size_t max_keys;   /* committee/key-cache capacity in keys (0 = default 16384) */
+    size_t max_keys;   /* key-cache capacity in keys (0 = fill a 96 GiB HBM budget) */
+    int key_window;    /* key comb window: 8, 12 or 16 bits (0 = auto at the first load: 16 for
+                          <= 384 keys, 12 for <= 12288 keys, else 8).  Table bytes per key:
+                          w8 0.53 MB, w12 5.77 MB, w16 67.1 MB; additions per signature 32/22/16 */
 } nw_opts;
 
 /* One certificate: its votes are sig[first_vote .. first_vote + n_votes). */

@@ -24,7 +24,8 @@ class DeviceError(RuntimeError):
 
 
 class NwOpts(ctypes.Structure):
-    _fields_ = [("device", ctypes.c_int), ("flags", ctypes.c_uint32), ("max_keys", ctypes.c_size_t)]
+    _fields_ = [("device", ctypes.c_int), ("flags", ctypes.c_uint32), ("max_keys", ctypes.c_size_t),
+                ("key_window", ctypes.c_int)]
 
 
 class NwCert(ctypes.Structure):
@@ -74,9 +75,9 @@ def _buf(b: bytes):
 class Engine:
     """One nw_ctx (one GPU).  Thread-safe: the C layer serializes calls on a context."""
 
-    def __init__(self, device: int = -1, max_keys: int = 0):
+    def __init__(self, device: int = -1, max_keys: int = 0, key_window: int = 0):
         self._ctx = ctypes.c_void_p()
-        opts = NwOpts(device, 0, max_keys)
+        opts = NwOpts(device, 0, max_keys, key_window)
         rc = LIB.nw_ctx_create(ctypes.byref(self._ctx), ctypes.byref(opts))
         if rc != NW_OK:
             raise DeviceError("nw_ctx_create failed (rc=%d): no usable gfx950 GPU" % rc)

@@ -52,7 +52,10 @@ struct nw_ctx {
     // basepoint comb
     uint32_t* d_btab = nullptr;
     // key cache
-    size_t max_keys = 16384;
+    size_t max_keys = 0;          // 0: derived from the HBM budget once the window is fixed
+    bool max_keys_user = false;
+    int key_window = 0;           // 0: not yet decided (first load)
+    size_t key_words = 0;         // u32 words per key table
     size_t nkeys = 0, key_cap = 0;
     uint32_t* d_keys_raw = nullptr;
     uint32_t* d_key_info = nullptr;
@@ -67,7 +70,7 @@ struct nw_ctx {
     // workspace
     DevBuf w_bases, w_sig, w_signer, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len,
         w_flags, w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_stake_out, w_ok, w_misc,
-        w_out;
+        w_out, w_pbuf, w_pre;
 };
 
 namespace {
@@ -90,6 +93,14 @@ const uint8_t kBaseEnc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x
                               0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                               0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
 
+constexpr size_t KEY_CACHE_BUDGET = 96ull << 30;   // bytes of HBM for key tables by default
+
+void fix_window(nw_ctx* ctx, size_t first_load) {
+    if (ctx->key_window == 0) ctx->key_window = first_load <= 384 ? 16 : (first_load <= 12288 ? 12 : 8);
+    ctx->key_words = comb_words(ctx->key_window);
+    if (!ctx->max_keys_user) ctx->max_keys = KEY_CACHE_BUDGET / (ctx->key_words * 4);
+}
+
 int grow_keys(nw_ctx* ctx, size_t need) {
     if (need <= ctx->key_cap) return NW_OK;
     if (need > ctx->max_keys) {
@@ -103,12 +114,12 @@ int grow_keys(nw_ctx* ctx, size_t need) {
     NW_TRY(hipMalloc(&raw, cap * 32), "hipMalloc(keys_raw)");
     NW_TRY(hipMalloc(&info, cap * 4), "hipMalloc(key_info)");
     NW_TRY(hipMalloc(&stake, cap * 4), "hipMalloc(stake)");
-    NW_TRY(hipMalloc(&tab, cap * (size_t)COMB_WORDS * 4), "hipMalloc(key_tab)");
+    NW_TRY(hipMalloc(&tab, cap * ctx->key_words * 4), "hipMalloc(key_tab)");
     if (ctx->nkeys) {
         NW_TRY(hipMemcpyAsync(raw, ctx->d_keys_raw, ctx->nkeys * 32, hipMemcpyDeviceToDevice, ctx->stream), "copy");
         NW_TRY(hipMemcpyAsync(info, ctx->d_key_info, ctx->nkeys * 4, hipMemcpyDeviceToDevice, ctx->stream), "copy");
         NW_TRY(hipMemcpyAsync(stake, ctx->d_stake, ctx->nkeys * 4, hipMemcpyDeviceToDevice, ctx->stream), "copy");
-        NW_TRY(hipMemcpyAsync(tab, ctx->d_key_tab, ctx->nkeys * (size_t)COMB_WORDS * 4, hipMemcpyDeviceToDevice,
+        NW_TRY(hipMemcpyAsync(tab, ctx->d_key_tab, ctx->nkeys * ctx->key_words * 4, hipMemcpyDeviceToDevice,
                               ctx->stream),
                "copy");
         NW_TRY(hipStreamSynchronize(ctx->stream), "sync");
@@ -126,13 +137,14 @@ int grow_keys(nw_ctx* ctx, size_t need) {
 }
 
 // Build tables for keys [k0, k0 + nk) whose raw bytes are already in d_keys_raw.
-int build_keys(nw_ctx* ctx, uint32_t* d_raw, uint32_t* d_info, uint32_t* d_tab, size_t nk) {
-    const size_t chunk = 4096;   // bounds the bases scratch (5 KB per key)
+int build_keys(nw_ctx* ctx, uint32_t* d_raw, uint32_t* d_info, uint32_t* d_tab, size_t nk, int window) {
+    const size_t chunk = window == 16 ? 64 : 4096;   // bounds the bases scratch and grid size
+    const size_t words = comb_words(window);
     for (size_t s = 0; s < nk; s += chunk) {
         const size_t m = nk - s < chunk ? nk - s : chunk;
-        NW_TRY(ctx->w_bases.ensure(m * COMB_POS * 40 * 4), "hipMalloc(bases)");
-        NW_TRY(launch_key_prep((uint32_t)m, d_raw + s * 8, d_info + s, ctx->w_bases.as<uint32_t>(),
-                               d_tab + s * (size_t)COMB_WORDS, ctx->stream),
+        NW_TRY(ctx->w_bases.ensure(m * comb_pos(window) * 40 * 4), "hipMalloc(bases)");
+        NW_TRY(launch_key_prep((uint32_t)m, d_raw + s * 8, d_info + s, ctx->w_bases.as<uint32_t>(), d_tab + s * words,
+                               window, ctx->stream),
                "k_key_prep/k_comb_entries");
     }
     return NW_OK;
@@ -166,6 +178,7 @@ int ensure_slots(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, si
         ctx->h_stake.push_back(stake ? stake[i] : 0u);
     }
     const size_t add = pending.size();
+    if (add && ctx->key_window == 0) fix_window(ctx, add);
     if (add) {
         int rc = grow_keys(ctx, ctx->nkeys + add);
         if (rc != NW_OK) {
@@ -175,8 +188,8 @@ int ensure_slots(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, si
         const size_t k0 = ctx->nkeys;
         NW_TRY(hipMemcpyAsync(ctx->d_keys_raw + k0 * 8, new_raw.data(), add * 32, hipMemcpyHostToDevice, ctx->stream),
                "H2D keys");
-        rc = build_keys(ctx, ctx->d_keys_raw + k0 * 8, ctx->d_key_info + k0, ctx->d_key_tab + k0 * (size_t)COMB_WORDS,
-                        add);
+        rc = build_keys(ctx, ctx->d_keys_raw + k0 * 8, ctx->d_key_info + k0, ctx->d_key_tab + k0 * ctx->key_words,
+                        add, ctx->key_window);
         if (rc != NW_OK) return rc;
         for (auto& kv : pending) ctx->slot_of.emplace(kv.first, kv.second);
         ctx->nkeys += add;
@@ -213,6 +226,8 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
     NW_TRY(ctx->w_slow_list.ensure(nsigs * 4 + 4), "ws slow_list");
     NW_TRY(ctx->w_slow_slot.ensure(nsigs * 4 + 4), "ws slow_slot");
     if (batch_mode) NW_TRY(ctx->w_slow_buf.ensure(nsigs * (size_t)SLOW_WORDS * 4 + 4), "ws slow_buf");
+    NW_TRY(ctx->w_pbuf.ensure(nsigs * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
+    NW_TRY(ctx->w_pre.ensure(nsigs * 40 + 16), "ws pre");
     NW_TRY(hipMemsetAsync(ctx->w_slow_count.p, 0, 16, st), "memset");
     // votes not covered by any certificate map to certificate 0 (never out of range)
     NW_TRY(hipMemsetAsync(ctx->w_sig_cert.p, 0, nsigs * 4 + 4, st), "memset sig_cert");
@@ -240,6 +255,8 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
     vp.slow_list = ctx->w_slow_list.as<uint32_t>();
     vp.slow_slot = ctx->w_slow_slot.as<uint32_t>();
     vp.slow_buf = ctx->w_slow_buf.as<uint32_t>();
+    vp.pbuf = ctx->w_pbuf.as<uint32_t>();
+    vp.pre = ctx->w_pre.as<uint32_t>();
     hipEvent_t ev_stop = nullptr;
     if (ctx->prof_on && nsigs) {
         if (ctx->prof_used == ctx->prof_events.size()) {
@@ -252,17 +269,12 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
         ev_stop = ctx->prof_events[ctx->prof_used].second;
         ++ctx->prof_used;
     }
-    NW_TRY(launch_verify(vp, msgmode, st), "k_verify");
+    NW_TRY(launch_verify(vp, msgmode, ctx->key_window, st), "k_verify");
+    NW_TRY(launch_finish(vp, st), "k_finish");
     if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");
     if (!batch_mode) return NW_OK;
 
-    SlowParams sp{};
-    sp.slow_count = vp.slow_count;
-    sp.slow_list = vp.slow_list;
-    sp.slow_buf = vp.slow_buf;
-    sp.sig = d_sig;
-    sp.flags = d_flags;
-    NW_TRY(launch_slow(sp, (uint32_t)nsigs, st), "k_slow_sig");
+    NW_TRY(launch_slow(vp, msgmode, ctx->key_window, (uint32_t)nsigs, st), "k_slow_sig");
 
     FinalizeParams fp{};
     fp.ncerts = (uint32_t)ncerts;
@@ -364,7 +376,18 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
         return NW_ERR_ARG;
     }
     ctx->device = dev;
-    if (opts && opts->max_keys) ctx->max_keys = opts->max_keys;
+    if (opts && opts->max_keys) {
+        ctx->max_keys = opts->max_keys;
+        ctx->max_keys_user = true;
+    }
+    if (opts && opts->key_window) {
+        if (opts->key_window != 8 && opts->key_window != 12 && opts->key_window != 16) {
+            delete ctx;
+            return NW_ERR_ARG;
+        }
+        ctx->key_window = opts->key_window;
+        fix_window(ctx, 0);
+    }
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return NW_ERR_DEVICE;
@@ -372,14 +395,14 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     // basepoint comb (one "key" = B)
     uint32_t* d_braw = nullptr;
     uint32_t* d_binfo = nullptr;
-    if (hipMalloc(&ctx->d_btab, (size_t)COMB_WORDS * 4) != hipSuccess || hipMalloc(&d_braw, 32) != hipSuccess ||
+    if (hipMalloc(&ctx->d_btab, comb_words(B_WINDOW) * 4) != hipSuccess || hipMalloc(&d_braw, 32) != hipSuccess ||
         hipMalloc(&d_binfo, 16) != hipSuccess) {
         nw_ctx_destroy(ctx);
         return NW_ERR_NOMEM;
     }
     int rc = NW_OK;
     if (hipMemcpy(d_braw, kBaseEnc, 32, hipMemcpyHostToDevice) != hipSuccess) rc = NW_ERR_DEVICE;
-    if (rc == NW_OK) rc = build_keys(ctx, d_braw, d_binfo, ctx->d_btab, 1);
+    if (rc == NW_OK) rc = build_keys(ctx, d_braw, d_binfo, ctx->d_btab, 1, B_WINDOW);
     if (rc == NW_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = NW_ERR_DEVICE;
     (void)hipFree(d_braw);
     (void)hipFree(d_binfo);
@@ -398,7 +421,7 @@ void nw_ctx_destroy(nw_ctx* ctx) {
     for (DevBuf* b : {&ctx->w_bases, &ctx->w_sig, &ctx->w_signer, &ctx->w_sig_cert, &ctx->w_cert_first, &ctx->w_cert_n,
                       &ctx->w_msg, &ctx->w_msg_off, &ctx->w_msg_len, &ctx->w_flags, &ctx->w_slow_count,
                       &ctx->w_slow_list, &ctx->w_slow_slot, &ctx->w_slow_buf, &ctx->w_cert_ok, &ctx->w_stake_out,
-                      &ctx->w_ok, &ctx->w_misc, &ctx->w_out})
+                      &ctx->w_ok, &ctx->w_misc, &ctx->w_out, &ctx->w_pbuf, &ctx->w_pre})
         b->release();
     for (auto& ev : ctx->prof_events) {
         (void)hipEventDestroy(ev.first);

@@ -94,32 +94,34 @@ NW_HD void hram_generic(uint32_t out[16], const uint32_t R[8], const uint32_t A[
     sha512_digest_le32(out, st);
 }
 
-// P = s B - h A via two signed radix-2^8 combs (32 positions each).
-template <bool WITH_A>
-NW_HD ge_p3 comb_sB_minus_hA(const uint32_t s_in[8], const uint32_t h_in[8],
-                                                  const uint32_t* __restrict__ btab,
-                                                  const uint32_t* __restrict__ atab) {
+// P = s B - h A: radix-2^WB comb over the basepoint table, then radix-2^WA comb over the key
+// table (WA = 0: s B only).  Both loops are rolled; each step is one gather + one mixed addition.
+template <int WB, int WA>
+NW_HD ge_p3 comb_sB_minus_hA(const uint32_t s_in[8], const uint32_t h_in[8], const uint32_t* __restrict__ btab,
+                             const uint32_t* __restrict__ atab) {
     uint32_t s[8], h[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         s[k] = s_in[k];
         h[k] = h_in[k];
     }
-    int cs = 0, ch = 0;
     ge_p3 P = ge_identity();
+    int cs = 0;
 #pragma nounroll
-    for (int pos = 0; pos < COMB_POS; ++pos) {
-        const int ds = next_digit256(s, cs);
-        const int as = ds < 0 ? -ds : ds;
-        const ge_precomp eb = load_precomp(btab + (size_t)(pos * COMB_ENT + as) * PRECOMP_WORDS);
-        if (WITH_A) {
-            const int dh = next_digit256(h, ch);
-            const int ah = dh < 0 ? -dh : dh;
-            const ge_precomp ea = load_precomp(atab + (size_t)(pos * COMB_ENT + ah) * PRECOMP_WORDS);
-            P = ge_madd(P, ge_precomp_cneg(eb, ds < 0));
-            P = ge_madd(P, ge_precomp_cneg(ea, dh > 0));   // -h A: negate for positive digits
-        } else {
-            P = ge_madd(P, ge_precomp_cneg(eb, ds < 0));
+    for (int pos = 0; pos < comb_pos(WB); ++pos) {
+        const int d = next_digit<WB>(s, cs);
+        const int ad = d < 0 ? -d : d;
+        const ge_precomp e = load_precomp(btab + ((size_t)pos * comb_ent(WB) + ad) * PRECOMP_WORDS);
+        P = ge_madd(P, ge_precomp_cneg(e, d < 0));
+    }
+    if constexpr (WA > 0) {
+        int ch = 0;
+#pragma nounroll
+        for (int pos = 0; pos < comb_pos(WA); ++pos) {
+            const int d = next_digit<WA>(h, ch);
+            const int ad = d < 0 ? -d : d;
+            const ge_precomp e = load_precomp(atab + ((size_t)pos * comb_ent(WA) + ad) * PRECOMP_WORDS);
+            P = ge_madd(P, ge_precomp_cneg(e, d > 0));   // -h A: negate for positive digits
         }
     }
     return P;
@@ -140,30 +142,60 @@ NW_HD void hram_msg32(uint32_t h[8], const uint32_t R[8], const uint32_t A[8], c
 }
 
 // P = s B - h A (s forced to 0 when non-canonical so the comb's digit range stays valid).
+template <int WA>
 NW_HD ge_p3 compute_P(const uint32_t S[8], const uint32_t h[8], bool sok, const uint32_t* btab,
                       const uint32_t* atab) {
     uint32_t s_use[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) s_use[k] = sok ? S[k] : 0u;
-    return comb_sB_minus_hA<true>(s_use, h, btab, atab);
+    return comb_sB_minus_hA<B_WINDOW, WA>(s_use, h, btab, atab);
 }
 
-// Flags from P (with zi = 1/Z_P) against the signature's R encoding:
+NW_HD fe load_fe(const uint32_t* p) {
+    fe f;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) f.v[k] = p[k];
+    return f;
+}
+
+NW_HD void store_fe(uint32_t* p, const fe& f) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) p[k] = f.v[k];
+}
+
+NW_HD void store_xyz(uint32_t* dst, const ge_p3& P) {
+    store_fe(dst, P.X);
+    store_fe(dst + 10, P.Y);
+    store_fe(dst + 20, P.Z);
+    dst[30] = 0;
+    dst[31] = 0;
+}
+
+// Completes the per-signature flags from P's projective X, Y and zi = 1/Z:
 //   MATCH  <=> R decodes (dalek decompress) and decode(R) == P  (the strict equation R = sB - hA)
 //   STRICT <=> verify_strict accepts (adds: S ok, A ok, neither R nor A of small order)
-NW_HD uint32_t match_flags(const ge_p3& P, const fe& zi, const uint32_t R[8], bool sok, bool aok, bool asmall) {
+NW_HD uint32_t finish_flags(const fe& X, const fe& Y, const fe& zi, const uint32_t R[8], uint32_t partial) {
     uint32_t xw[8], yw[8];
-    fe_tobytes_w(xw, fe_mul(P.X, zi));
-    fe_tobytes_w(yw, fe_mul(P.Y, zi));
+    fe_tobytes_w(xw, fe_mul(X, zi));
+    fe_tobytes_w(yw, fe_mul(Y, zi));
     // R's y (bit 255 cleared) reduced mod p, as FieldElement::from_bytes reads it
     uint32_t yr[8];
     fe_tobytes_w(yr, fe_frombytes_w(R));
     const bool x_zero = (xw[0] | xw[1] | xw[2] | xw[3] | xw[4] | xw[5] | xw[6] | xw[7]) == 0;
     const bool match = words_eq8(yw, yr) && (x_zero || ((xw[0] & 1u) == (R[7] >> 31)));
     const bool rsmall = y_is_small_order(yw);
+    const bool sok = (partial & NW_F_S_OK) != 0, aok = (partial & NW_F_A_OK) != 0;
+    const bool asmall = (partial & NW_F_A_SMALL) != 0;
     const bool strict = sok && aok && match && !asmall && !rsmall;
-    return (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | (match ? NW_F_MATCH : 0u) |
-           (strict ? NW_F_STRICT : 0u) | (asmall ? NW_F_A_SMALL : 0u) | (rsmall ? NW_F_R_SMALL : 0u);
+    return partial | (match ? NW_F_MATCH : 0u) | (strict ? NW_F_STRICT : 0u) | (rsmall ? NW_F_R_SMALL : 0u);
+}
+
+// Flags from P (with zi = 1/Z_P) against the signature's R encoding:
+//   MATCH  <=> R decodes (dalek decompress) and decode(R) == P  (the strict equation R = sB - hA)
+//   STRICT <=> verify_strict accepts (adds: S ok, A ok, neither R nor A of small order)
+NW_HD uint32_t match_flags(const ge_p3& P, const fe& zi, const uint32_t R[8], bool sok, bool aok, bool asmall) {
+    return finish_flags(P.X, P.Y, zi, R,
+                        (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | (asmall ? NW_F_A_SMALL : 0u));
 }
 
 // Torsion coefficient of signature i: ((r - z h) mod 8) * t mod 8 with r = z h mod l
@@ -192,9 +224,10 @@ NW_HD ge_p3 ge_t8() {
     return T8;
 }
 
-// Key cache preparation for one key: returns key_info bits and writes the 32 comb bases
-// 256^pos * A (extended, 40 words each).  Undecodable keys use the identity (their verdicts are
+// Key cache preparation for one key: returns key_info bits and writes the comb bases
+// 2^(W pos) * A (extended, 40 words each).  Undecodable keys use the identity (their verdicts are
 // Err regardless) so every table entry stays a valid curve point.
+template <int W>
 NW_HD uint32_t key_prep_one(const uint32_t* raw, uint32_t* bases) {
     uint32_t w[8];
     load_w8(w, raw);
@@ -212,14 +245,15 @@ NW_HD uint32_t key_prep_one(const uint32_t* raw, uint32_t* bases) {
         Q = ge_add(Q, t8c);
     }
     ge_p3 cur = A;
-    for (int pos = 0; pos < COMB_POS; ++pos) {
+    for (int pos = 0; pos < comb_pos(W); ++pos) {
         store_p3(bases + (size_t)pos * 40, cur);
-        for (int d = 0; d < 8; ++d) cur = ge_dbl(cur);
+        for (int d = 0; d < W; ++d) cur = ge_dbl(cur);
     }
     return (ok ? KI_OK : 0u) | (small ? KI_SMALL : 0u) | (t << KI_TORSION_SHIFT);
 }
 
-// Comb entry e (0..128) of position pos: e * 256^pos * A in affine Niels form.
+// Comb entry e (0..2^(W-1)) of position pos: e * 2^(W pos) * A in affine Niels form.
+template <int W>
 NW_HD void comb_entry_one(const uint32_t* bases, uint32_t pos, uint32_t e, uint32_t* tab) {
     ge_precomp q;
     if (e == 0) {
@@ -228,13 +262,13 @@ NW_HD void comb_entry_one(const uint32_t* bases, uint32_t pos, uint32_t e, uint3
         const ge_p3 base = load_p3(bases + (size_t)pos * 40);
         const ge_cached bc = ge_to_cached(base);
         ge_p3 acc = ge_identity();
-        for (int b = 7; b >= 0; --b) {
+        for (int b = W - 1; b >= 0; --b) {
             acc = ge_dbl(acc);
             if ((e >> b) & 1u) acc = ge_add(acc, bc);
         }
         q = ge_to_precomp(acc);
     }
-    uint32_t* dst = tab + (size_t)(pos * COMB_ENT + e) * PRECOMP_WORDS;
+    uint32_t* dst = tab + ((size_t)pos * comb_ent(W) + e) * PRECOMP_WORDS;
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
         dst[k] = q.ypx.v[k];
@@ -269,7 +303,7 @@ NW_HD void sign_one(const uint32_t* seed_in, const uint32_t* msg_in, const uint3
     sc_reduce512(ared, wide);
     uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t Aw[8];
-    ge_compress_w(Aw, comb_sB_minus_hA<false>(ared, zero8, btab, nullptr));
+    ge_compress_w(Aw, comb_sB_minus_hA<B_WINDOW, 0>(ared, zero8, btab, nullptr));
     uint32_t pm[8 + MW];
 #pragma unroll
     for (int k = 0; k < 8; ++k) pm[k] = hs[8 + k];
@@ -280,7 +314,7 @@ NW_HD void sign_one(const uint32_t* seed_in, const uint32_t* msg_in, const uint3
     uint32_t r[8];
     sc_reduce512(r, rh);
     uint32_t Rw[8];
-    ge_compress_w(Rw, comb_sB_minus_hA<false>(r, zero8, btab, nullptr));
+    ge_compress_w(Rw, comb_sB_minus_hA<B_WINDOW, 0>(r, zero8, btab, nullptr));
     uint32_t ram[16 + MW];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {

@@ -11,7 +11,9 @@ static constexpr uint32_t KI_OK = 1u;             // decodes (dalek::PublicKey::
 static constexpr uint32_t KI_SMALL = 2u;          // small order
 static constexpr uint32_t KI_TORSION_SHIFT = 4;   // 3 bits: t with A^t = t * T8
 static constexpr uint32_t NW_F_TCOEF_SHIFT = 8;   // 3 bits of per-signature torsion coefficient
-static constexpr int SLOW_WORDS = 48;             // slow-path record: point (40 words) + z (4) + pad
+static constexpr int SLOW_WORDS = 40;             // slow-path record: extended point z_i (R_i - P_i)
+static constexpr int PBUF_WORDS = 32;             // per-signature P record: X, Y, Z (30 words) + pad
+static constexpr int FINISH_K = 16;               // signatures per lane in the batch-inversion kernel
 
 struct VerifyParams {
     uint32_t n;                    // signatures
@@ -27,22 +29,16 @@ struct VerifyParams {
     uint64_t cert_base;            // global index of certificate 0 (z stream nonce)
     const uint32_t* keys_raw;      // [K][8] raw key words (as hashed)
     const uint32_t* key_info;      // [K]
-    const uint32_t* key_tab;       // [K][COMB_WORDS]
-    const uint32_t* btab;          // [COMB_WORDS] basepoint comb
+    const uint32_t* key_tab;       // [K][comb_words(key_window)]
+    const uint32_t* btab;          // [comb_words(16)] basepoint comb
     uint32_t zseed[8];
     uint32_t* flags;               // [n] NW_F_* bits
     uint32_t* slow_count;          // [1]
     uint32_t* slow_list;           // [n]
     uint32_t* slow_slot;           // [n]
     uint32_t* slow_buf;            // [n][SLOW_WORDS]
-};
-
-struct SlowParams {
-    const uint32_t* slow_count;
-    const uint32_t* slow_list;
-    uint32_t* slow_buf;
-    const uint8_t* sig;
-    uint32_t* flags;
+    uint32_t* pbuf;                // [n][PBUF_WORDS]  P_i = s_i B - h_i A_i (X, Y, Z)
+    uint32_t* pre;                 // [n][10]          prefix products of Z (k_finish scratch)
 };
 
 struct FinalizeParams {
@@ -58,14 +54,15 @@ struct FinalizeParams {
     uint64_t* accepted_stake;      // [ncerts] (may be null)
 };
 
-hipError_t launch_verify(const VerifyParams& p, int msgmode, hipStream_t st);
-hipError_t launch_slow(const SlowParams& p, uint32_t n_upper, hipStream_t st);
+hipError_t launch_verify(const VerifyParams& p, int msgmode, int key_window, hipStream_t st);
+hipError_t launch_finish(const VerifyParams& p, hipStream_t st);
+hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st);
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st);
 hipError_t launch_expand_certs(uint32_t ncerts, const uint32_t* first, const uint32_t* nv, uint32_t* sig_cert,
                                hipStream_t st);
 hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hipStream_t st);
 hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
-                           uint32_t* tab, hipStream_t st);
+                           uint32_t* tab, int window, hipStream_t st);
 hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                               uint8_t* out, hipStream_t st);
 hipError_t launch_sign(uint32_t n, int msg_words, const uint32_t* seeds, const uint32_t* msgs,

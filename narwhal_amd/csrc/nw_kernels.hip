@@ -1,10 +1,10 @@
 // gfx950 kernels for the Ed25519 verify + SHA-512 hot path.
 //
 // Verification strategy: for signature i with committee key A_i,
-//     P_i = s_i B - h_i A_i          (two fixed-base combs, 64 mixed additions, no doublings)
-// is compared with the signature's R encoding after ONE wave-batched inversion.  P_i == R_i is
-// exactly dalek's strict equation (verify_strict).  The cofactorless batch equation of
-// dalek::verify_batch with coefficients z_i,
+//     P_i = s_i B - h_i A_i          (two fixed-base combs, 32 mixed additions, no doublings)
+// is compared with the signature's R encoding.  P_i == decode(R_i) is exactly dalek's strict
+// equation (verify_strict).  The cofactorless batch equation of dalek::verify_batch with
+// coefficients z_i,
 //     sum_i [ z_i R_i + (z_i h_i mod l) A_i ] - (sum_i z_i s_i mod l) B == O,
 // decomposes exactly (with D_i = R_i - P_i, A_i^t the 8-torsion part of A_i, l = 5 mod 8) into
 //     sum_i z_i D_i  +  sum_i ((r_i - z_i h_i) mod 8) A_i^t == O,      r_i = z_i h_i mod l,
@@ -12,6 +12,10 @@
 // without any variable-base work; everything else goes to the exact path (k_slow_sig), which
 // evaluates the remaining terms literally.  Verdicts are therefore identical to dalek's for every
 // input (not just honest ones) given the same z_i.
+//
+// Pipeline per batch: k_expand_certs -> k_verify (P_i, one lane per signature) -> k_finish
+// (Montgomery batch inversion of Z over chunks of FINISH_K signatures per lane, encoding match,
+// strict verdict) -> k_slow_sig (compacted list of mismatches only) -> k_cert_finalize.
 #include <hip/hip_runtime.h>
 #include "nw_point.h"
 #include "nw_sha512.h"
@@ -21,74 +25,17 @@
 
 namespace nw {
 
-// ------------------------------------------------------------------------------------ wave helpers
-__device__ __forceinline__ fe shfl_fe(const fe& a, int src) {
-    fe r;
-#pragma unroll
-    for (int k = 0; k < 10; ++k) r.v[k] = (uint32_t)__shfl((int)a.v[k], src, 64);
-    return r;
-}
-
-__device__ __forceinline__ fe shfl_up_fe(const fe& a, unsigned d) {
-    fe r;
-#pragma unroll
-    for (int k = 0; k < 10; ++k) r.v[k] = (uint32_t)__shfl_up((int)a.v[k], d, 64);
-    return r;
-}
-
-__device__ __forceinline__ fe shfl_down_fe(const fe& a, unsigned d) {
-    fe r;
-#pragma unroll
-    for (int k = 0; k < 10; ++k) r.v[k] = (uint32_t)__shfl_down((int)a.v[k], d, 64);
-    return r;
-}
-
-// Montgomery's trick across the 64 lanes of a wave: every lane gets 1/z_lane for the cost of
-// one inversion per wave plus two log-depth product scans.  All 64 lanes must call it.
-__device__ fe wave_batch_invert(const fe& z) {
-    const int lane = threadIdx.x & 63;
-    const fe one = fe_one();
-    fe pre = z;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        fe t = shfl_up_fe(pre, off);
-        t = fe_select(t, one, lane < off);
-        pre = fe_mul(pre, t);
-    }
-    fe suf = z;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        fe t = shfl_down_fe(suf, off);
-        t = fe_select(t, one, lane + off >= 64);
-        suf = fe_mul(suf, t);
-    }
-    const fe inv_all = fe_invert(shfl_fe(pre, 63));
-    fe pre_ex = shfl_up_fe(pre, 1);
-    pre_ex = fe_select(pre_ex, one, lane == 0);
-    fe suf_ex = shfl_down_fe(suf, 1);
-    suf_ex = fe_select(suf_ex, one, lane == 63);
-    return fe_mul(fe_mul(inv_all, pre_ex), suf_ex);
-}
-
-// ------------------------------------------------------------------------------------ verify
+// Signature i's inputs and h = SHA-512(R || A || M) mod l.
 template <int MSGMODE>
-__global__ void __launch_bounds__(256) k_verify(VerifyParams a) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = gid < a.n;
-    const uint32_t i = live ? gid : a.n - 1;
-
-    uint32_t R[8], S[8], Aw[8];
+__device__ __forceinline__ void lane_inputs(const VerifyParams& a, uint32_t i, uint32_t R[8], uint32_t S[8],
+                                            uint32_t& slot, uint32_t& kinfo, uint32_t& cert, uint32_t h[8]) {
+    uint32_t Aw[8];
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
     load_w8(S, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16 + 8);
-    const uint32_t slot = a.signer[i];
+    slot = a.signer[i];
     load_w8(Aw, a.keys_raw + (size_t)slot * 8);
-    const uint32_t kinfo = a.key_info[slot];
-    const uint32_t cert = a.sig_cert[i];
-
-    const bool sok = sc_is_canonical(S);
-    const bool aok = (kinfo & KI_OK) != 0;
-
-    uint32_t h[8];
+    kinfo = a.key_info[slot];
+    cert = a.sig_cert[i];
     if (MSGMODE == 0) {
         uint32_t M[8];
         load_w8(M, reinterpret_cast<const uint32_t*>(a.cert_msg) + (size_t)cert * 8);
@@ -98,54 +45,91 @@ __global__ void __launch_bounds__(256) k_verify(VerifyParams a) {
         hram_generic(hw, R, Aw, a.msg_base + a.msg_off[i], a.msg_len[i]);
         sc_reduce512(h, hw);
     }
+}
 
-    const ge_p3 P = compute_P(S, h, sok, a.btab, a.key_tab + (size_t)slot * COMB_WORDS);
+__device__ __forceinline__ void coeff_z(const VerifyParams& a, uint32_t i, uint32_t cert, uint32_t z4[4]) {
+    const uint64_t bidx = a.cert_base + cert;
+    chacha20_z(z4, a.zseed, i - a.cert_first[cert], (uint32_t)bidx, (uint32_t)(bidx >> 32), 0u);
+}
 
-    // affine P via one inversion per wave
-    const fe zi = wave_batch_invert(live ? P.Z : fe_one());
-    uint32_t flags = match_flags(P, zi, R, sok, aok, (kinfo & KI_SMALL) != 0);
-    const bool match = (flags & NW_F_MATCH) != 0;
-
-    if (a.batch_mode && live) {
-        const uint32_t tk = (kinfo >> KI_TORSION_SHIFT) & 7u;
-        const bool need_z = sok && aok && (!match || tk != 0);
-        if (need_z) {
-            uint32_t z4[4];
-            const uint64_t bidx = a.cert_base + cert;
-            chacha20_z(z4, a.zseed, i - a.cert_first[cert], (uint32_t)bidx, (uint32_t)(bidx >> 32), 0u);
-            if (tk != 0) flags |= torsion_coef(z4, h, tk) << NW_F_TCOEF_SHIFT;
-            if (!match) {
-                flags |= NW_F_SLOW;
-                const uint32_t slot_out = atomicAdd(a.slow_count, 1u);
-                a.slow_list[slot_out] = i;
-                a.slow_slot[i] = slot_out;
-                uint32_t* dst = a.slow_buf + (size_t)slot_out * SLOW_WORDS;
-                store_p3(dst, P);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) dst[40 + k] = z4[k];
-            }
-        }
+// ------------------------------------------------------------------------------------ verify (P_i)
+// One lane per signature: P_i = s_i B - h_i A_i, written as (X, Y, Z) to pbuf; partial flags
+// (S ok, A ok, A small, torsion coefficient for torsion keys).
+template <int MSGMODE, int WA>
+__global__ void __launch_bounds__(256) k_verify(VerifyParams a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    uint32_t R[8], S[8], h[8], slot, kinfo, cert;
+    lane_inputs<MSGMODE>(a, i, R, S, slot, kinfo, cert, h);
+    const bool sok = sc_is_canonical(S);
+    const bool aok = (kinfo & KI_OK) != 0;
+    const ge_p3 P = compute_P<WA>(S, h, sok, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
+    store_xyz(a.pbuf + (size_t)i * PBUF_WORDS, P);
+    uint32_t flags = (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | ((kinfo & KI_SMALL) ? NW_F_A_SMALL : 0u);
+    const uint32_t tk = (kinfo >> KI_TORSION_SHIFT) & 7u;
+    if (a.batch_mode && tk != 0 && sok && aok) {
+        uint32_t z4[4];
+        coeff_z(a, i, cert, z4);
+        flags |= torsion_coef(z4, h, tk) << NW_F_TCOEF_SHIFT;
     }
-    if (live) a.flags[i] = flags;
+    a.flags[i] = flags;
+}
+
+// ------------------------------------------------------------------------------------ finish
+// One lane per chunk of FINISH_K consecutive signatures: Montgomery batch inversion of their Z
+// (one field inversion per chunk), affine x, y, encoding match against R, strict verdict, and
+// (batch mode) compaction of the mismatching signatures into the exact-path list.
+__global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
+    const uint64_t L = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t s0 = L * FINISH_K;
+    if (s0 >= a.n) return;
+    const uint32_t cnt = (uint32_t)((a.n - s0) < FINISH_K ? (a.n - s0) : FINISH_K);
+    fe acc = fe_one();
+    for (uint32_t k = 0; k < cnt; ++k) {
+        acc = fe_mul(acc, load_fe(a.pbuf + (s0 + k) * PBUF_WORDS + 20));
+        store_fe(a.pre + (s0 + k) * 10, acc);
+    }
+    fe inv = fe_invert(acc);
+    for (int k = (int)cnt - 1; k >= 0; --k) {
+        const uint64_t i = s0 + k;
+        const uint32_t* pb = a.pbuf + i * PBUF_WORDS;
+        fe zi = inv;
+        if (k > 0) {
+            zi = fe_mul(inv, load_fe(a.pre + (i - 1) * 10));
+            inv = fe_mul(inv, load_fe(pb + 20));
+        }
+        uint32_t R[8];
+        load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + i * 16);
+        uint32_t f = finish_flags(load_fe(pb), load_fe(pb + 10), zi, R, a.flags[i]);
+        if (a.batch_mode && (f & (NW_F_S_OK | NW_F_A_OK)) == (NW_F_S_OK | NW_F_A_OK) && !(f & NW_F_MATCH)) {
+            f |= NW_F_SLOW;
+            const uint32_t t = atomicAdd(a.slow_count, 1u);
+            a.slow_list[t] = (uint32_t)i;
+            a.slow_slot[i] = t;
+        }
+        a.flags[i] = f;
+    }
 }
 
 // Exact path for signatures with D_i != O: Q_i = z_i (R_i - P_i); R decode failure -> F_R_BAD.
-__global__ void __launch_bounds__(256) k_slow_sig(SlowParams a) {
+template <int MSGMODE, int WA>
+__global__ void __launch_bounds__(256) k_slow_sig(VerifyParams a) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= *a.slow_count) return;
     const uint32_t i = a.slow_list[t];
     uint32_t* buf = a.slow_buf + (size_t)t * SLOW_WORDS;
-    uint32_t R[8];
-    load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
+    uint32_t R[8], S[8], h[8], slot, kinfo, cert;
+    lane_inputs<MSGMODE>(a, i, R, S, slot, kinfo, cert, h);
     ge_p3 Rp;
-    const bool rok = ge_decompress(Rp, R);
-    if (!rok) {
+    if (!ge_decompress(Rp, R)) {
         a.flags[i] |= NW_F_R_BAD;
         store_p3(buf, ge_identity());
         return;
     }
-    uint32_t z[4] = {buf[40], buf[41], buf[42], buf[43]};
-    store_p3(buf, slow_term(Rp, load_p3(buf), z));
+    const ge_p3 P = compute_P<WA>(S, h, true, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
+    uint32_t z4[4];
+    coeff_z(a, i, cert, z4);
+    store_p3(buf, slow_term(Rp, P, z4));
 }
 
 // Per-certificate verdict: definitive Err on any bad S / undecodable A / undecodable R, else the
@@ -200,23 +184,25 @@ __global__ void __launch_bounds__(256) k_flags_to_ok(uint32_t n, const uint32_t*
 }
 
 // ------------------------------------------------------------------------------------ key cache
-// One thread per key: decode, small-order flag, torsion index, comb bases 256^i A.
+// One thread per key: decode, small-order flag, torsion index, comb bases 2^(W i) A.
+template <int W>
 __global__ void __launch_bounds__(64) k_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info,
                                                  uint32_t* bases) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= nk) return;
-    key_info[j] = key_prep_one(keys_raw + (size_t)j * 8, bases + (size_t)j * COMB_POS * 40);
+    key_info[j] = key_prep_one<W>(keys_raw + (size_t)j * 8, bases + (size_t)j * comb_pos(W) * 40);
 }
 
-// One thread per (key, position, entry): entry e of position pos = e * 256^pos * A, affine Niels.
+// One thread per (key, position, entry): entry e of position pos = e * 2^(W pos) * A, affine Niels.
+template <int W>
 __global__ void __launch_bounds__(256) k_comb_entries(uint32_t nk, const uint32_t* bases, uint32_t* tab) {
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t per_key = (uint64_t)COMB_POS * COMB_ENT;
+    const uint64_t per_key = (uint64_t)comb_pos(W) * comb_ent(W);
     if (gid >= (uint64_t)nk * per_key) return;
     const uint32_t j = (uint32_t)(gid / per_key);
     const uint32_t rem = (uint32_t)(gid % per_key);
-    comb_entry_one(bases + (size_t)j * COMB_POS * 40, rem / COMB_ENT, rem % COMB_ENT,
-                   tab + (size_t)j * COMB_WORDS);
+    comb_entry_one<W>(bases + (size_t)j * comb_pos(W) * 40, rem / comb_ent(W), rem % comb_ent(W),
+                      tab + (size_t)j * comb_words(W));
 }
 
 // ------------------------------------------------------------------------------------ SHA-512 bulk
@@ -299,19 +285,51 @@ __global__ void __launch_bounds__(256) k_sign(uint32_t n, const uint32_t* seeds,
 // ------------------------------------------------------------------------------------ launchers
 static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 
-hipError_t launch_verify(const VerifyParams& p, int msgmode, hipStream_t st) {
-    if (p.n == 0) return hipSuccess;
+template <int MSGMODE>
+static void launch_verify_w(const VerifyParams& p, int wa, bool slow, uint32_t n_upper, hipStream_t st) {
+    const dim3 b(256);
+    const dim3 g(blocks_for(slow ? n_upper : p.n, 256));
+    switch (wa) {
+        case 8:
+            if (slow) hipLaunchKernelGGL((k_slow_sig<MSGMODE, 8>), g, b, 0, st, p);
+            else hipLaunchKernelGGL((k_verify<MSGMODE, 8>), g, b, 0, st, p);
+            break;
+        case 12:
+            if (slow) hipLaunchKernelGGL((k_slow_sig<MSGMODE, 12>), g, b, 0, st, p);
+            else hipLaunchKernelGGL((k_verify<MSGMODE, 12>), g, b, 0, st, p);
+            break;
+        default:
+            if (slow) hipLaunchKernelGGL((k_slow_sig<MSGMODE, 16>), g, b, 0, st, p);
+            else hipLaunchKernelGGL((k_verify<MSGMODE, 16>), g, b, 0, st, p);
+            break;
+    }
+}
+
+static hipError_t launch_vs(const VerifyParams& p, int msgmode, int key_window, bool slow, uint32_t n_upper,
+                            hipStream_t st) {
+    if (key_window != 8 && key_window != 12 && key_window != 16) return hipErrorInvalidValue;
     if (msgmode == 0)
-        hipLaunchKernelGGL(k_verify<0>, dim3(blocks_for(p.n, 256)), dim3(256), 0, st, p);
+        launch_verify_w<0>(p, key_window, slow, n_upper, st);
     else
-        hipLaunchKernelGGL(k_verify<1>, dim3(blocks_for(p.n, 256)), dim3(256), 0, st, p);
+        launch_verify_w<1>(p, key_window, slow, n_upper, st);
     return hipGetLastError();
 }
 
-hipError_t launch_slow(const SlowParams& p, uint32_t n_upper, hipStream_t st) {
-    if (n_upper == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_slow_sig, dim3(blocks_for(n_upper, 256)), dim3(256), 0, st, p);
+hipError_t launch_verify(const VerifyParams& p, int msgmode, int key_window, hipStream_t st) {
+    if (p.n == 0) return hipSuccess;
+    return launch_vs(p, msgmode, key_window, false, 0, st);
+}
+
+hipError_t launch_finish(const VerifyParams& p, hipStream_t st) {
+    if (p.n == 0) return hipSuccess;
+    const uint64_t lanes = (p.n + FINISH_K - 1) / FINISH_K;
+    hipLaunchKernelGGL(k_finish, dim3(blocks_for(lanes, 256)), dim3(256), 0, st, p);
     return hipGetLastError();
+}
+
+hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st) {
+    if (n_upper == 0) return hipSuccess;
+    return launch_vs(p, msgmode, key_window, true, n_upper, st);
 }
 
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
@@ -334,15 +352,26 @@ hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hi
     return hipGetLastError();
 }
 
-hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
-                           uint32_t* tab, hipStream_t st) {
-    if (nk == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_key_prep, dim3(blocks_for(nk, 64)), dim3(64), 0, st, nk, keys_raw, key_info, bases);
+template <int W>
+static hipError_t launch_key_prep_w(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
+                                    uint32_t* tab, hipStream_t st) {
+    hipLaunchKernelGGL(k_key_prep<W>, dim3(blocks_for(nk, 64)), dim3(64), 0, st, nk, keys_raw, key_info, bases);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const uint64_t total = (uint64_t)nk * COMB_POS * COMB_ENT;
-    hipLaunchKernelGGL(k_comb_entries, dim3(blocks_for(total, 256)), dim3(256), 0, st, nk, bases, tab);
+    const uint64_t total = (uint64_t)nk * comb_pos(W) * comb_ent(W);
+    hipLaunchKernelGGL(k_comb_entries<W>, dim3(blocks_for(total, 256)), dim3(256), 0, st, nk, bases, tab);
     return hipGetLastError();
+}
+
+hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
+                           uint32_t* tab, int window, hipStream_t st) {
+    if (nk == 0) return hipSuccess;
+    switch (window) {
+        case 8: return launch_key_prep_w<8>(nk, keys_raw, key_info, bases, tab, st);
+        case 12: return launch_key_prep_w<12>(nk, keys_raw, key_info, bases, tab, st);
+        case 16: return launch_key_prep_w<16>(nk, keys_raw, key_info, bases, tab, st);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off, const uint64_t* len,

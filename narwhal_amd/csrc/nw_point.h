@@ -25,10 +25,14 @@ struct ge_cached {
 // Table entry layout in HBM: 32 u32 words = 128 B (one cache line):
 //   [0..9] y+x, [10..19] y-x, [20..29] 2dxy, [30..31] zero pad.
 static constexpr int PRECOMP_WORDS = 32;
-// Fixed-base comb: 32 positions of signed radix-2^8 digits, entries |d| = 0..128 (0 = identity).
-static constexpr int COMB_POS = 32;
-static constexpr int COMB_ENT = 129;
-static constexpr int COMB_WORDS = COMB_POS * COMB_ENT * PRECOMP_WORDS;   // per point (528,384 B)
+// Fixed-base combs: signed radix-2^W digits, one table per digit position holding the multiples
+// |d| * 2^(W*pos) * P for |d| = 0..2^(W-1) (0 = identity).  W = 16 for the basepoint (67 MB,
+// shared by every signature); W = 8 / 12 / 16 for committee keys, chosen by committee size so the
+// key cache fits HBM (nw_opts.key_window).  Additions per scalar = ceil(256 / W); no doublings.
+NW_HD constexpr int comb_pos(int w) { return (256 + w - 1) / w; }
+NW_HD constexpr int comb_ent(int w) { return (1 << (w - 1)) + 1; }
+NW_HD constexpr size_t comb_words(int w) { return (size_t)comb_pos(w) * comb_ent(w) * PRECOMP_WORDS; }
+static constexpr int B_WINDOW = 16;
 
 NW_HD ge_p3 ge_identity() {
     ge_p3 r;
@@ -221,15 +225,16 @@ NW_HD ge_precomp ge_to_precomp(const ge_p3& p) {
     return q;
 }
 
-// Signed radix-2^8 recoding, consumed one digit per call: s holds the remaining scalar bits
-// (8 LE words, value < 2^253 so the top digit needs no carry-out).  Returns d in [-128, 128].
-NW_HD int next_digit256(uint32_t s[8], int& carry) {
-    const int b = (int)(s[0] & 0xFFu) + carry;
-    carry = (b + 128) >> 8;
-    const int d = b - (carry << 8);
+// Signed radix-2^W recoding, consumed one digit per call: s holds the remaining scalar bits
+// (8 LE words, value < 2^253 so the top digit never carries out).  Returns d in [-2^(W-1), 2^(W-1)].
+template <int W>
+NW_HD int next_digit(uint32_t s[8], int& carry) {
+    const int b = (int)(s[0] & ((1u << W) - 1u)) + carry;
+    carry = (b + (1 << (W - 1))) >> W;
+    const int d = b - (carry << W);
 #pragma unroll
-    for (int k = 0; k < 7; ++k) s[k] = (s[k] >> 8) | (s[k + 1] << 24);
-    s[7] >>= 8;
+    for (int k = 0; k < 7; ++k) s[k] = (s[k] >> W) | (s[k + 1] << (32 - W));
+    s[7] >>= W;
     return d;
 }
 

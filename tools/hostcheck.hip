@@ -23,6 +23,21 @@ static void fe_out(uint8_t* b, const fe& f) {
     w2b(b, w);
 }
 
+template <int W>
+static uint32_t build_comb_w(const uint32_t raw[8], uint32_t* bases, uint32_t* tab) {
+    const uint32_t info = key_prep_one<W>(raw, bases);
+    for (uint32_t pos = 0; pos < (uint32_t)comb_pos(W); ++pos)
+        for (uint32_t e = 0; e < (uint32_t)comb_ent(W); ++e) comb_entry_one<W>(bases, pos, e, tab);
+    return info;
+}
+
+template <int W>
+static ge_p3 compute_P_w(int w, const uint32_t S[8], const uint32_t h[8], bool sok, const uint32_t* btab,
+                         const uint32_t* atab) {
+    (void)w;
+    return compute_P<W>(S, h, sok, btab, atab);
+}
+
 extern "C" {
 
 void hc_fe_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { fe_out(out, fe_mul(fe_in(a), fe_in(b))); }
@@ -107,21 +122,20 @@ void hc_point_ops(const uint8_t* a, const uint8_t* b, const uint8_t* k, uint8_t*
 }
 
 // Build the comb table of one key exactly as k_key_prep + k_comb_entries do.
-uint32_t hc_build_comb(const uint8_t* key, uint32_t* tab /* COMB_WORDS */) {
+uint32_t hc_build_comb(const uint8_t* key, uint32_t* tab, int w) {
     uint32_t raw[8];
     b2w(raw, key);
-    std::vector<uint32_t> bases(COMB_POS * 40);
-    const uint32_t info = key_prep_one(raw, bases.data());
-    for (uint32_t pos = 0; pos < (uint32_t)COMB_POS; ++pos)
-        for (uint32_t e = 0; e < (uint32_t)COMB_ENT; ++e) comb_entry_one(bases.data(), pos, e, tab);
-    return info;
+    std::vector<uint32_t> bases(comb_pos(w) * 40);
+    if (w == 8) return build_comb_w<8>(raw, bases.data(), tab);
+    if (w == 12) return build_comb_w<12>(raw, bases.data(), tab);
+    return build_comb_w<16>(raw, bases.data(), tab);
 }
-size_t hc_comb_words(void) { return (size_t)COMB_WORDS; }
+size_t hc_comb_words(int w) { return comb_words(w); }
 
 // One signature through the verify lane math (single-lane inversion instead of the wave trick).
 // Returns the NW_F_* flags (+ torsion coefficient bits when zseed != NULL).
 uint32_t hc_verify_lane(const uint8_t* sig64, const uint8_t* pk, const uint8_t* msg, uint64_t len, uint32_t kinfo,
-                        const uint32_t* atab, const uint32_t* btab, const uint8_t* zseed, uint32_t counter,
+                        const uint32_t* atab, int wa, const uint32_t* btab, const uint8_t* zseed, uint32_t counter,
                         uint64_t bidx, uint8_t* slow_q /* 32 B compressed z(R-P) or zeros */, int* rbad) {
     uint32_t R[8], S[8], A[8];
     b2w(R, sig64);
@@ -139,7 +153,9 @@ uint32_t hc_verify_lane(const uint8_t* sig64, const uint8_t* pk, const uint8_t* 
         hram_generic(hw, R, A, msg, len);
         sc_reduce512(h, hw);
     }
-    const ge_p3 P = compute_P(S, h, sok, btab, atab);
+    const ge_p3 P = wa == 8 ? compute_P_w<8>(wa, S, h, sok, btab, atab)
+                            : (wa == 12 ? compute_P_w<12>(wa, S, h, sok, btab, atab)
+                                        : compute_P_w<16>(wa, S, h, sok, btab, atab));
     uint32_t flags = match_flags(P, fe_invert(P.Z), R, sok, aok, (kinfo & KI_SMALL) != 0);
     *rbad = 0;
     std::memset(slow_q, 0, 32);

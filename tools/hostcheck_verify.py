@@ -15,28 +15,30 @@ lib = ctypes.CDLL(os.path.join(HERE, "libhostcheck.so"))
 lib.hc_comb_words.restype = ctypes.c_size_t
 lib.hc_build_comb.restype = ctypes.c_uint32
 lib.hc_verify_lane.restype = ctypes.c_uint32
-NW = lib.hc_comb_words()
+lib.hc_comb_words.argtypes = [ctypes.c_int]
+KEY_W = int(os.environ.get("KEY_W", "8"))
 F_S_OK, F_A_OK, F_MATCH, F_STRICT, F_SLOW = 1, 2, 4, 8, 0x1000
 
 _tabs = {}
 
 
-def comb(key):
-    if key not in _tabs:
-        tab = (ctypes.c_uint32 * NW)()
-        info = lib.hc_build_comb(key, tab)
-        _tabs[key] = (tab, info)
-    return _tabs[key]
+def comb(key, w=None):
+    w = w or KEY_W
+    if (key, w) not in _tabs:
+        tab = (ctypes.c_uint32 * lib.hc_comb_words(w))()
+        info = lib.hc_build_comb(key, tab, w)
+        _tabs[(key, w)] = (tab, info)
+    return _tabs[(key, w)]
 
 
-BTAB, _ = comb(o.pt_compress(o.B_POINT))
+BTAB, _ = comb(o.pt_compress(o.B_POINT), 16)
 
 
 def lane(sig, pk, msg, zseed, counter, bidx):
     tab, info = comb(pk)
     q = ctypes.create_string_buffer(32)
     rbad = ctypes.c_int(0)
-    f = lib.hc_verify_lane(sig, pk, msg, ctypes.c_uint64(len(msg)), info, tab, BTAB, zseed, counter,
+    f = lib.hc_verify_lane(sig, pk, msg, ctypes.c_uint64(len(msg)), info, tab, KEY_W, BTAB, zseed, counter,
                            ctypes.c_uint64(bidx), q, ctypes.byref(rbad))
     return f, q.raw, rbad.value
 
