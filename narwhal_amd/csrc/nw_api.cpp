@@ -70,7 +70,7 @@ struct nw_ctx {
     // workspace
     DevBuf w_bases, w_sig, w_signer, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len,
         w_flags, w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_stake_out, w_ok, w_misc,
-        w_out, w_pbuf, w_pre;
+        w_out, w_pbuf, w_pre, w_counts, w_cursor, w_perm;
 };
 
 namespace {
@@ -94,6 +94,7 @@ const uint8_t kBaseEnc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x
                               0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
 
 constexpr size_t KEY_CACHE_BUDGET = 96ull << 30;   // bytes of HBM for key tables by default
+constexpr size_t kGroupMinSigs = 16384;            // group signatures by signer above this batch size
 
 void fix_window(nw_ctx* ctx, size_t first_load) {
     if (ctx->key_window == 0) ctx->key_window = first_load <= 384 ? 16 : (first_load <= 12288 ? 12 : 8);
@@ -257,6 +258,16 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
     vp.slow_buf = ctx->w_slow_buf.as<uint32_t>();
     vp.pbuf = ctx->w_pbuf.as<uint32_t>();
     vp.pre = ctx->w_pre.as<uint32_t>();
+    vp.perm = nullptr;
+    if (nsigs >= kGroupMinSigs && ctx->nkeys > 1) {
+        NW_TRY(ctx->w_counts.ensure(ctx->nkeys * 4 + 16), "ws counts");
+        NW_TRY(ctx->w_cursor.ensure(ctx->nkeys * 4 + 16), "ws cursor");
+        NW_TRY(ctx->w_perm.ensure(nsigs * 4 + 16), "ws perm");
+        NW_TRY(launch_group_by_signer((uint32_t)nsigs, (uint32_t)ctx->nkeys, d_signer, ctx->w_counts.as<uint32_t>(),
+                                      ctx->w_cursor.as<uint32_t>(), ctx->w_perm.as<uint32_t>(), st),
+               "signer grouping");
+        vp.perm = ctx->w_perm.as<uint32_t>();
+    }
     hipEvent_t ev_stop = nullptr;
     if (ctx->prof_on && nsigs) {
         if (ctx->prof_used == ctx->prof_events.size()) {
@@ -421,7 +432,8 @@ void nw_ctx_destroy(nw_ctx* ctx) {
     for (DevBuf* b : {&ctx->w_bases, &ctx->w_sig, &ctx->w_signer, &ctx->w_sig_cert, &ctx->w_cert_first, &ctx->w_cert_n,
                       &ctx->w_msg, &ctx->w_msg_off, &ctx->w_msg_len, &ctx->w_flags, &ctx->w_slow_count,
                       &ctx->w_slow_list, &ctx->w_slow_slot, &ctx->w_slow_buf, &ctx->w_cert_ok, &ctx->w_stake_out,
-                      &ctx->w_ok, &ctx->w_misc, &ctx->w_out, &ctx->w_pbuf, &ctx->w_pre})
+                      &ctx->w_ok, &ctx->w_misc, &ctx->w_out, &ctx->w_pbuf, &ctx->w_pre,
+                      &ctx->w_counts, &ctx->w_cursor, &ctx->w_perm})
         b->release();
     for (auto& ev : ctx->prof_events) {
         (void)hipEventDestroy(ev.first);

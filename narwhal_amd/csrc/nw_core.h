@@ -94,8 +94,46 @@ NW_HD void hram_generic(uint32_t out[16], const uint32_t R[8], const uint32_t A[
     sha512_digest_le32(out, st);
 }
 
+// One comb pass: P += sum_pos sign(d_pos) * T[pos][|d_pos|] for the signed radix-2^W digits of
+// sc (consumed).  Software-pipelined: the gather of position pos+1's entry is issued before the
+// mixed addition of position pos, so the (HBM / Infinity-Cache) latency hides under ~1.3k VALU
+// instructions of field arithmetic.  neg_pos: negate entries for positive digits (-h A).
+template <int W>
+NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab, bool neg_pos) {
+    int carry = 0;
+    int d = next_digit<W>(sc, carry);
+    const uint4* q = reinterpret_cast<const uint4*>(tab + (size_t)(d < 0 ? -d : d) * PRECOMP_WORDS);
+    uint4 cur[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cur[k] = q[k];
+#pragma nounroll
+    for (int pos = 0; pos < comb_pos(W); ++pos) {
+        uint4 nxt[8];
+        int dn = 0;
+        if (pos + 1 < comb_pos(W)) {
+            dn = next_digit<W>(sc, carry);
+            const uint4* qn = reinterpret_cast<const uint4*>(
+                tab + ((size_t)(pos + 1) * comb_ent(W) + (dn < 0 ? -dn : dn)) * PRECOMP_WORDS);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) nxt[k] = qn[k];
+        }
+        uint32_t w[32];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            w[4 * k] = cur[k].x;
+            w[4 * k + 1] = cur[k].y;
+            w[4 * k + 2] = cur[k].z;
+            w[4 * k + 3] = cur[k].w;
+        }
+        P = ge_madd(P, ge_precomp_cneg(ge_precomp_from_words(w), neg_pos ? d > 0 : d < 0));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
+        d = dn;
+    }
+}
+
 // P = s B - h A: radix-2^WB comb over the basepoint table, then radix-2^WA comb over the key
-// table (WA = 0: s B only).  Both loops are rolled; each step is one gather + one mixed addition.
+// table (WA = 0: s B only).  Each step is one gather + one mixed addition, no doublings.
 template <int WB, int WA>
 NW_HD ge_p3 comb_sB_minus_hA(const uint32_t s_in[8], const uint32_t h_in[8], const uint32_t* __restrict__ btab,
                              const uint32_t* __restrict__ atab) {
@@ -106,24 +144,8 @@ NW_HD ge_p3 comb_sB_minus_hA(const uint32_t s_in[8], const uint32_t h_in[8], con
         h[k] = h_in[k];
     }
     ge_p3 P = ge_identity();
-    int cs = 0;
-#pragma nounroll
-    for (int pos = 0; pos < comb_pos(WB); ++pos) {
-        const int d = next_digit<WB>(s, cs);
-        const int ad = d < 0 ? -d : d;
-        const ge_precomp e = load_precomp(btab + ((size_t)pos * comb_ent(WB) + ad) * PRECOMP_WORDS);
-        P = ge_madd(P, ge_precomp_cneg(e, d < 0));
-    }
-    if constexpr (WA > 0) {
-        int ch = 0;
-#pragma nounroll
-        for (int pos = 0; pos < comb_pos(WA); ++pos) {
-            const int d = next_digit<WA>(h, ch);
-            const int ad = d < 0 ? -d : d;
-            const ge_precomp e = load_precomp(atab + ((size_t)pos * comb_ent(WA) + ad) * PRECOMP_WORDS);
-            P = ge_madd(P, ge_precomp_cneg(e, d > 0));   // -h A: negate for positive digits
-        }
-    }
+    comb_pass<WB>(P, s, btab, false);
+    if constexpr (WA > 0) comb_pass<WA>(P, h, atab, true);
     return P;
 }
 

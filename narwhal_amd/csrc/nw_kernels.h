@@ -39,6 +39,7 @@ struct VerifyParams {
     uint32_t* slow_buf;            // [n][SLOW_WORDS]
     uint32_t* pbuf;                // [n][PBUF_WORDS]  P_i = s_i B - h_i A_i (X, Y, Z)
     uint32_t* pre;                 // [n][10]          prefix products of Z (k_finish scratch)
+    const uint32_t* perm;          // [n] processing order for k_verify (signer-grouped) or null
 };
 
 struct FinalizeParams {
@@ -56,6 +57,8 @@ struct FinalizeParams {
 
 hipError_t launch_verify(const VerifyParams& p, int msgmode, int key_window, hipStream_t st);
 hipError_t launch_finish(const VerifyParams& p, hipStream_t st);
+hipError_t launch_group_by_signer(uint32_t n, uint32_t nkeys, const uint32_t* signer, uint32_t* counts,
+                                  uint32_t* cursor, uint32_t* perm, hipStream_t st);
 hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st);
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st);
 hipError_t launch_expand_certs(uint32_t ncerts, const uint32_t* first, const uint32_t* nv, uint32_t* sig_cert,

@@ -57,22 +57,62 @@ __device__ __forceinline__ void coeff_z(const VerifyParams& a, uint32_t i, uint3
 // (S ok, A ok, A small, torsion coefficient for torsion keys).
 template <int MSGMODE, int WA>
 __global__ void __launch_bounds__(256) k_verify(VerifyParams a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= a.n) return;
+    // signer-grouped order: the 64 lanes of a wave mostly share one key table (TLB / cache locality)
+    const uint32_t i = a.perm ? a.perm[gid] : gid;
     uint32_t R[8], S[8], h[8], slot, kinfo, cert;
     lane_inputs<MSGMODE>(a, i, R, S, slot, kinfo, cert, h);
     const bool sok = sc_is_canonical(S);
     const bool aok = (kinfo & KI_OK) != 0;
-    const ge_p3 P = compute_P<WA>(S, h, sok, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
-    store_xyz(a.pbuf + (size_t)i * PBUF_WORDS, P);
     uint32_t flags = (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | ((kinfo & KI_SMALL) ? NW_F_A_SMALL : 0u);
     const uint32_t tk = (kinfo >> KI_TORSION_SHIFT) & 7u;
-    if (a.batch_mode && tk != 0 && sok && aok) {
+    if (a.batch_mode && tk != 0 && sok && aok) {   // torsion keys only (never for honest committees)
         uint32_t z4[4];
         coeff_z(a, i, cert, z4);
         flags |= torsion_coef(z4, h, tk) << NW_F_TCOEF_SHIFT;
     }
     a.flags[i] = flags;
+    const ge_p3 P = compute_P<WA>(S, h, sok, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
+    store_xyz(a.pbuf + (size_t)i * PBUF_WORDS, P);
+}
+
+// ------------------------------------------------------------------------------------ signer grouping
+// Counting sort of signature indices by key-cache slot: perm lists the signatures of slot 0, then
+// slot 1, ...  (order inside a slot is arbitrary; every output is written at the original index).
+__global__ void __launch_bounds__(256) k_count_slots(uint32_t n, const uint32_t* signer, uint32_t* counts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&counts[signer[i]], 1u);
+}
+
+// Single-block exclusive scan of counts[0..k) into cursor[0..k).
+__global__ void __launch_bounds__(1024) k_scan_slots(uint32_t k, const uint32_t* counts, uint32_t* cursor) {
+    __shared__ uint32_t part[1024];
+    const uint32_t t = threadIdx.x;
+    const uint32_t per = (k + 1023) / 1024;
+    const uint32_t b = t * per, e = min(k, b + per);
+    uint32_t sum = 0;
+    for (uint32_t j = b; j < e; ++j) sum += counts[j];
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < 1024; off <<= 1) {
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - sum;   // exclusive prefix of this thread's chunk
+    for (uint32_t j = b; j < e; ++j) {
+        const uint32_t c = counts[j];
+        cursor[j] = run;
+        run += c;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_scatter_slots(uint32_t n, const uint32_t* signer, uint32_t* cursor,
+                                                       uint32_t* perm) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) perm[atomicAdd(&cursor[signer[i]], 1u)] = i;
 }
 
 // ------------------------------------------------------------------------------------ finish
@@ -318,6 +358,17 @@ static hipError_t launch_vs(const VerifyParams& p, int msgmode, int key_window, 
 hipError_t launch_verify(const VerifyParams& p, int msgmode, int key_window, hipStream_t st) {
     if (p.n == 0) return hipSuccess;
     return launch_vs(p, msgmode, key_window, false, 0, st);
+}
+
+hipError_t launch_group_by_signer(uint32_t n, uint32_t nkeys, const uint32_t* signer, uint32_t* counts,
+                                  uint32_t* cursor, uint32_t* perm, hipStream_t st) {
+    if (n == 0 || nkeys == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(counts, 0, (size_t)nkeys * 4, st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_count_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, signer, counts);
+    hipLaunchKernelGGL(k_scan_slots, dim3(1), dim3(1024), 0, st, nkeys, counts, cursor);
+    hipLaunchKernelGGL(k_scatter_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, signer, cursor, perm);
+    return hipGetLastError();
 }
 
 hipError_t launch_finish(const VerifyParams& p, hipStream_t st) {
