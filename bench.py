@@ -1,14 +1,20 @@
 """Benchmark: Ed25519 certificate verification throughput on MI355X (BASELINE.json metric).
 
-Workload (per GPU, weak scaling): BASELINE config C2 — a 100-validator committee and 14,926
-certificates x 67 votes = 1,000,042 signatures, inputs resident in HBM.  One "step" = one full
-pass of the hot path over that batch: per-vote strict verdicts + per-certificate batch verdicts +
-accepted stake (nw_verify_certs_dev), then (N > 1) an RCCL all-gather of the per-shard verdict
-bitmaps and stake tallies — the only collective the path has.
+Workload (per GPU, weak scaling): BASELINE config C2 (``configs[1]``) — a 100-validator committee
+and 14,926 certificates x 67 votes = 1,000,042 signatures, inputs resident in HBM.  One "step" =
+one full pass of the hot path over that batch: per-vote strict verdicts + per-certificate batch
+verdicts + accepted stake (nw_verify_certs_dev), then (N > 1) an RCCL all-gather of the per-shard
+verdict bitmaps and stake tallies — the only collective the path has.
 
-Prints ONE JSON line (rank 0).  ``roofline`` is for the dominant kernel (k_verify), timed with
-HIP events recorded by libnwcrypto on the launch stream; ``cpu_baseline`` times the oracle's C
-restatement of dalek's batch verify (oracle/, "port") on a bounded sample of the same workload.
+Prints ONE JSON line (rank 0):
+  * ``roofline`` — the dominant kernel, k_verify, timed with HIP events that libnwcrypto records on
+    the launch stream around each k_verify launch (nw_profile_*).  ``achieved`` = the kernel's
+    algorithmic u32 multiply-accumulates per launch (work model below) / average launch time;
+    ``peak`` = the measured v_mad_u64_u32 rate (tools/valu_peak.hip -> profiles/r01_valu_peak.json).
+  * ``cpu_baseline`` — the oracle's C restatement of dalek 1.0.1 (oracle/nw_ref.c, "port") timed on
+    the host cores on a bounded sample of the same certificates.
+  * ``digest`` — the worker's bulk SHA-512 (worker/src/processor.rs:65) over the C4 batch shape
+    (bincode batches of 977 x 512-B transactions), GPU vs hashlib on one host core.
 """
 import argparse
 import json
@@ -20,9 +26,24 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "Ed25519 sigs verified/s (node, 1/2/4/8 GPU); p50 latency per 2f+1 certificate"
-# SURVEY.md §8(d) cost model v1 (frozen): FM per signature at n votes per certificate, 100 u32 MADs per FM
-COST_MODEL_FM = {3: 1750, 67: 1030, 667: 811, 977: 775, 6667: 644}
-MADS_PER_FM = 100
+# SURVEY.md §8(d) cost model v1 (frozen): FM per signature of dalek's algorithm at n votes per
+# certificate (Straus / Pippenger MSM + R decompression).  Reported as ``dalek_equiv`` only: the
+# kernel runs a different (cheaper) algorithm, so v1 is not its work.
+COST_MODEL_V1_FM = {3: 1750, 67: 1030, 667: 811, 977: 775, 6667: 644}
+MADS_PER_FM = 100          # 10 x 10 radix-2^25.5 limb products per field multiplication
+B_WINDOW = 16              # basepoint comb window (nw_point.h)
+MADD_FM = 7                # mixed (affine Niels) addition = 7 field multiplications
+
+
+def comb_pos(w):
+    return (256 + w - 1) // w
+
+
+def kverify_fm_per_sig(key_window):
+    """k_verify's field multiplications per signature: one mixed addition per comb digit position
+    of s (basepoint comb) and of h (key comb); no doublings (nw_core.h comb_sB_minus_hA).  The
+    SHA-512 block, mod-l reduction and digit recoding are VALU work not counted here."""
+    return MADD_FM * (comb_pos(B_WINDOW) + comb_pos(key_window))
 
 
 def valu_peak_mad_per_s():
@@ -37,7 +58,7 @@ def valu_peak_mad_per_s():
 
 
 def traffic_per_launch():
-    """HBM bytes per k_verify launch from the committed rocprofv3 PMC pass (or None)."""
+    """HBM bytes per k_verify launch from the committed rocprofv3 PMC passes (or None)."""
     path = os.path.join(ROOT, "profiles", "traffic_k_verify.json")
     if not os.path.exists(path):
         return None
@@ -47,45 +68,99 @@ def traffic_per_launch():
 
 def cpu_baseline(cs, com, seconds):
     """Oracle restatement timed on host cores (rank 0, N = 1 only): bounded sample of certificates."""
-    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    try:
-        import nw_ref   # C port of dalek's u64 backend (oracle/nw_ref.c)
-        kind, impl = "port", "oracle/nw_ref.c (C restatement of ed25519-dalek 1.0.1 u64 backend)"
-    except ImportError:
-        nw_ref = None
-        kind, impl = "port", "oracle/ed25519_oracle.py (pure Python)"
+    import nw_ref   # C restatement of dalek's u64 backend (oracle/nw_ref.c); test/baseline only
     threads = int(os.environ.get("NW_CPU_THREADS", "16"))
     zseed = bytes(32)
-    done_sigs = 0
-    done_certs = 0
+    done_sigs = done_certs = 0
+    per_call = 64
+    c = 0
     t0 = time.perf_counter()
-    if nw_ref is not None:
-        # batches of certificates handed to the multi-threaded C verifier until the budget is spent
-        per_call = 64
-        c = 0
-        while time.perf_counter() - t0 < seconds:
-            sel = [(c + k) % cs.ncerts for k in range(per_call)]
-            ok = nw_ref.verify_certs(cs, com, sel, zseed, threads)
-            assert all(ok), "CPU baseline rejected an honest certificate"
-            done_certs += len(sel)
-            done_sigs += int(sum(int(cs.cert_n[x]) for x in sel))
-            c += per_call
-        cores = threads
-    else:
-        import ed25519_oracle as o
-        while time.perf_counter() - t0 < seconds:
-            c = done_certs % cs.ncerts
-            f, n = int(cs.cert_first[c]), int(cs.cert_n[c])
-            votes = [(bytes(com.pks[cs.signer[f + v]]), bytes(cs.sigs[f + v])) for v in range(n)]
-            assert o.crypto_verify_batch(bytes(cs.msgs[c]), votes, zseed, c)
-            done_certs += 1
-            done_sigs += n
-        cores = 1
+    while time.perf_counter() - t0 < seconds:
+        sel = [(c + k) % cs.ncerts for k in range(per_call)]
+        ok = nw_ref.verify_certs(cs, com, sel, zseed, threads)
+        assert all(ok), "CPU baseline rejected an honest certificate"
+        done_certs += len(sel)
+        done_sigs += int(sum(int(cs.cert_n[x]) for x in sel))
+        c += per_call
     dt = time.perf_counter() - t0
-    return {"value": done_sigs / dt, "unit": "sigs/s", "cores": cores, "kind": kind,
-            "sample": "%d certificates x %d votes of the C2 workload (%d sigs) in %.1f s; %s" % (
-                done_certs, int(cs.cert_n[0]), done_sigs, dt, impl)}
+    return {"value": done_sigs / dt, "unit": "sigs/s", "cores": threads, "kind": "port",
+            "sample": "%d certificates x %d votes of the C2 workload (%d sigs) in %.1f s on %d threads; "
+                      "oracle/nw_ref.c (C restatement of ed25519-dalek 1.0.1 u64 backend: per-vote A "
+                      "decompression + Straus MSM, as crypto/src/lib.rs:206-219)"
+                      % (done_certs, int(cs.cert_n[0]), done_sigs, dt, threads)}
+
+
+def digest_leg(eng, dev, n_batches, reps, cpu_seconds):
+    """Worker batch digests: SHA-512 of n_batches bincode batches resident in HBM (one lane per
+    batch: each batch is one sequential compression chain), plus the saturated kernel rate on
+    many short messages and hashlib on one host core."""
+    import hashlib
+    import numpy as np
+    import torch
+    from narwhal_amd import workload
+    out = {}
+    host = workload.worker_batches_np(n_batches)
+    blen = host.shape[1]
+    d_data = torch.from_numpy(host.reshape(-1)).to(dev)
+    d_off = torch.arange(n_batches, dtype=torch.int64, device=dev) * blen
+    d_len = torch.full((n_batches,), blen, dtype=torch.int64, device=dev)
+    d_out = torch.empty((n_batches, 64), dtype=torch.uint8, device=dev)
+
+    def run(nb, d_data, d_off, d_len, d_out, reps):
+        st = torch.cuda.current_stream()
+        eng.sha512_many_dev(d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), nb, d_out.data_ptr(),
+                            st.cuda_stream)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            eng.sha512_many_dev(d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), nb, d_out.data_ptr(),
+                                st.cuda_stream)
+        e1.record(st)
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) / reps / 1e3
+
+    t = run(n_batches, d_data, d_off, d_len, d_out, reps)
+    padded = n_batches * ((blen + 17 + 127) // 128) * 128
+    got = d_out[:4].cpu().numpy()
+    for b in range(4):
+        assert bytes(got[b]) == hashlib.sha512(host[b].tobytes()).digest(), "GPU batch digest mismatch"
+    out["workload"] = "%d worker batches x %d B (977 x 512-B tx, bincode WorkerMessage::Batch)" % (n_batches, blen)
+    out["GBps"] = n_batches * blen / t / 1e9
+    out["batches_per_s"] = n_batches / t
+    out["kernel_ms"] = t * 1e3
+    out["roofline_hbm"] = {"achieved": padded / t / 1e9, "peak": 8000.0, "unit": "GB/s",
+                           "frac": padded / t / 1e9 / 8000.0}
+    del d_data, d_off, d_len, d_out
+    # saturated rate: 2^21 independent 1 KiB messages (enough concurrent chains to fill every SIMD)
+    ns, ml = 1 << 21, 1024
+    g = torch.Generator(device="cpu").manual_seed(7)
+    small = torch.randint(0, 256, (ns * ml,), dtype=torch.uint8, generator=g)
+    d_small = small.to(dev)
+    s_off = torch.arange(ns, dtype=torch.int64, device=dev) * ml
+    s_len = torch.full((ns,), ml, dtype=torch.int64, device=dev)
+    s_out = torch.empty((ns, 64), dtype=torch.uint8, device=dev)
+    ts = run(ns, d_small, s_off, s_len, s_out, reps)
+    chk = s_out[:2].cpu().numpy()
+    sm = small[:2 * ml].numpy()
+    for b in range(2):
+        assert bytes(chk[b]) == hashlib.sha512(sm[b * ml:(b + 1) * ml].tobytes()).digest()
+    out["valu_ceiling_GBps"] = ns * ((ml + 17 + 127) // 128) * 128 / ts / 1e9
+    out["roofline_valu"] = {"achieved": out["roofline_hbm"]["achieved"], "peak": out["valu_ceiling_GBps"],
+                            "unit": "GB/s", "frac": out["roofline_hbm"]["achieved"] / out["valu_ceiling_GBps"],
+                            "note": "peak = same kernel on 2^21 x 1 KiB messages (saturated SHA-512 VALU rate)"}
+    del d_small, s_off, s_len, s_out
+    if cpu_seconds > 0:
+        t0 = time.perf_counter()
+        nb = 0
+        while time.perf_counter() - t0 < cpu_seconds:
+            hashlib.sha512(host[nb % n_batches].tobytes()).digest()
+            nb += 1
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"GBps": nb * blen / dt / 1e9, "cores": 1, "kind": "hashlib (OpenSSL) SHA-512",
+                               "sample": "%d batches in %.1f s" % (nb, dt)}
+    return out
 
 
 def main():
@@ -99,6 +174,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-samples", type=int, default=200)
+    ap.add_argument("--digest-batches", type=int, default=10000, help="0 disables the digest leg")
     args = ap.parse_args()
 
     import numpy as np
@@ -112,7 +188,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from narwhal_amd import _lib, workload
+    from narwhal_amd import _lib, shard, workload
     eng = _lib.Engine(device=local)
     com = workload.make_committee(args.validators, eng)
     slots = eng.committee_load_np(com.pks, com.stake)
@@ -128,7 +204,6 @@ def main():
     d_ok = torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev)
     d_flags = torch.zeros(cs.nsigs, dtype=torch.int32, device=dev)
     d_stake = torch.zeros(cs.ncerts, dtype=torch.int64, device=dev)
-    from narwhal_amd import shard
     ranges = [(r * args.certs, (r + 1) * args.certs) for r in range(world)]   # node-wide certificate ranges
     zseed = os.urandom(32)
 
@@ -143,7 +218,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ok_all = bool(d_ok.all().item())
+    ok_all = bool(d_ok.all().item()) and bool((d_stake == args.votes).all().item())
     if world > 1:
         dist.barrier()
     eng.profile_read()             # discard warmup events
@@ -172,19 +247,25 @@ def main():
     total_sigs = world * cs.nsigs * args.steps
     value = total_sigs / elapsed
 
-    out = None
     if rank == 0:
-        # roofline of k_verify (cost model v1 algorithmic MADs / measured launch time)
         avg_launch_s = (kms / kn) / 1e3 if kn else float("nan")
-        fm = COST_MODEL_FM.get(args.votes)
-        achieved = (cs.nsigs * fm * MADS_PER_FM / avg_launch_s) / 1e12 if fm else None
+        kw = eng.key_window()
+        fm = kverify_fm_per_sig(kw)
         peak = valu_peak_mad_per_s() / 1e12
-        traffic = traffic_per_launch()
-        roofline = {"bound": "valu", "kernel": "k_verify", "achieved": achieved, "peak": peak, "unit": "TMAD/s",
-                    "frac": (achieved / peak) if achieved else None, "traffic": traffic,
-                    "avg_launch_ms": avg_launch_s * 1e3, "launches": kn,
-                    "note": "achieved = sigs/launch x %s FM/sig (SURVEY §8(d) cost model v1, n=%d) x 100 u32 "
-                            "MADs / avg k_verify time; peak = measured v_mad_u64_u32 rate" % (fm, args.votes)}
+        achieved = cs.nsigs * fm * MADS_PER_FM / avg_launch_s / 1e12
+        v1 = COST_MODEL_V1_FM.get(args.votes)
+        roofline = {
+            "bound": "valu", "kernel": "k_verify", "achieved": achieved, "peak": peak, "unit": "TMAD/s",
+            "frac": achieved / peak, "traffic": traffic_per_launch(),
+            "avg_launch_ms": avg_launch_s * 1e3, "launches": kn,
+            "work_model": "%d sigs/launch x %d FM/sig (7 FM per mixed addition x (%d basepoint + %d key) comb "
+                          "positions, key window %d) x 100 u32 MADs; SHA-512/mod-l/recoding VALU work not counted; "
+                          "peak = measured v_mad_u64_u32 rate" % (cs.nsigs, fm, comb_pos(B_WINDOW), comb_pos(kw), kw),
+            "dalek_equiv": {"fm_per_sig": v1, "TMADps": (cs.nsigs * v1 * MADS_PER_FM / avg_launch_s / 1e12)
+                            if v1 else None,
+                            "note": "SURVEY §8(d) cost model v1 = dalek's MSM work per signature; the comb "
+                                    "algorithm needs %.1fx fewer FM" % (v1 / fm) if v1 else ""},
+        }
         # single-certificate latency (H2D -> kernels -> D2H), the Core::run usage pattern
         lat = []
         for i in range(args.latency_samples):
@@ -204,14 +285,20 @@ def main():
             "config": {"workload": "C2: %d-validator committee, %d certificates x %d votes (%d sigs) per GPU"
                                    % (args.validators, args.certs, args.votes, cs.nsigs),
                        "validators": args.validators, "certs_per_gpu": args.certs, "votes_per_cert": args.votes,
+                       "key_window": kw,
                        "parallelism": "certificate shards per GPU; RCCL all_gather of verdict bitmaps + stake"},
-            "p50_cert_latency_ms": lat[len(lat) // 2] * 1e3, "p99_cert_latency_ms": lat[int(len(lat) * 0.99)] * 1e3,
+            "p50_cert_latency_ms": lat[len(lat) // 2] * 1e3 if lat else None,
+            "p99_cert_latency_ms": lat[int(len(lat) * 0.99)] * 1e3 if lat else None,
             "roofline": roofline,
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cs, com, args.cpu_seconds)
         else:
             out["cpu_baseline"] = None
+        if world == 1 and args.digest_batches > 0:
+            del d_sig, d_signer, d_flags
+            out["digest"] = digest_leg(eng, dev, args.digest_batches, 3,
+                                       0.0 if args.no_cpu_baseline else 3.0)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

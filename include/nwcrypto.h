@@ -74,6 +74,8 @@ int nw_committee_load(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stak
                       uint32_t* slot_out);
 /* Number of cached keys. */
 size_t nw_committee_size(const nw_ctx* ctx);
+/* Key comb window in use (8 / 12 / 16; 0 before the first load). */
+int nw_key_window(const nw_ctx* ctx);
 
 /* ---- verification ----------------------------------------------------------------------------
  * crypto::Signature::verify (crypto/src/lib.rs:200-204): strict single verify of ``msg``. */

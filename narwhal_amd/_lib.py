@@ -44,6 +44,7 @@ def _load() -> ctypes.CDLL:
         "nw_last_error": (ctypes.c_char_p, [P]),
         "nw_committee_load": (I, [P, P, P, S, P]),
         "nw_committee_size": (S, [P]),
+        "nw_key_window": (I, [P]),
         "nw_verify_strict": (I, [P, P, S, P, P]),
         "nw_verify_strict_many": (I, [P, P, P, P, P, S, P]),
         "nw_verify_batch": (I, [P, P, P, P, P, S, P, U64]),
@@ -120,6 +121,9 @@ class Engine:
 
     def committee_size(self) -> int:
         return LIB.nw_committee_size(self._ctx)
+
+    def key_window(self) -> int:
+        return LIB.nw_key_window(self._ctx)
 
     # -- verification -------------------------------------------------------------------------
     def verify_strict(self, msg: bytes, pk: bytes, sig: bytes) -> bool:

@@ -281,8 +281,8 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
         ++ctx->prof_used;
     }
     NW_TRY(launch_verify(vp, msgmode, ctx->key_window, st), "k_verify");
+    if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");   // brackets k_verify alone
     NW_TRY(launch_finish(vp, st), "k_finish");
-    if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");
     if (!batch_mode) return NW_OK;
 
     NW_TRY(launch_slow(vp, msgmode, ctx->key_window, (uint32_t)nsigs, st), "k_slow_sig");
@@ -472,6 +472,8 @@ int nw_profile_read(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launc
 const char* nw_last_error(const nw_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
 
 size_t nw_committee_size(const nw_ctx* ctx) { return ctx ? ctx->nkeys : 0; }
+
+int nw_key_window(const nw_ctx* ctx) { return ctx ? ctx->key_window : 0; }
 
 int nw_committee_load(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, size_t n, uint32_t* slot_out) {
     if (!ctx || (!pk && n)) return NW_ERR_ARG;

@@ -185,6 +185,26 @@ NW_HD void store_fe(uint32_t* p, const fe& f) {
     for (int k = 0; k < 10; ++k) p[k] = f.v[k];
 }
 
+// Struct-of-arrays field element: limb k of column g at p[k * n + g].
+NW_HD fe load_fe_soa(const uint32_t* p, size_t n, size_t g) {
+    fe f;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) f.v[k] = p[k * n + g];
+    return f;
+}
+
+NW_HD void store_fe_soa(uint32_t* p, size_t n, size_t g, const fe& f) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) p[k * n + g] = f.v[k];
+}
+
+// P's X, Y, Z as 30 SoA rows (X rows 0..9, Y 10..19, Z 20..29).
+NW_HD void store_xyz_soa(uint32_t* p, size_t n, size_t g, const ge_p3& P) {
+    store_fe_soa(p, n, g, P.X);
+    store_fe_soa(p + 10 * n, n, g, P.Y);
+    store_fe_soa(p + 20 * n, n, g, P.Z);
+}
+
 NW_HD void store_xyz(uint32_t* dst, const ge_p3& P) {
     store_fe(dst, P.X);
     store_fe(dst + 10, P.Y);

@@ -37,8 +37,8 @@ struct VerifyParams {
     uint32_t* slow_list;           // [n]
     uint32_t* slow_slot;           // [n]
     uint32_t* slow_buf;            // [n][SLOW_WORDS]
-    uint32_t* pbuf;                // [n][PBUF_WORDS]  P_i = s_i B - h_i A_i (X, Y, Z)
-    uint32_t* pre;                 // [n][10]          prefix products of Z (k_finish scratch)
+    uint32_t* pbuf;                // [30][n] SoA, processing order: P = s B - h A (X, Y, Z rows)
+    uint32_t* pre;                 // [10][n] SoA prefix products of Z (k_finish scratch)
     const uint32_t* perm;          // [n] processing order for k_verify (signer-grouped) or null
 };
 

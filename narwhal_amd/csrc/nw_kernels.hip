@@ -13,8 +13,8 @@
 // evaluates the remaining terms literally.  Verdicts are therefore identical to dalek's for every
 // input (not just honest ones) given the same z_i.
 //
-// Pipeline per batch: k_expand_certs -> k_verify (P_i, one lane per signature) -> k_finish
-// (Montgomery batch inversion of Z over chunks of FINISH_K signatures per lane, encoding match,
+// Pipeline per batch: k_expand_certs -> [signer grouping] -> k_verify (P_i, one lane per signature)
+// -> k_finish (Montgomery batch inversion of Z over FINISH_K signatures per lane, encoding match,
 // strict verdict) -> k_slow_sig (compacted list of mismatches only) -> k_cert_finalize.
 #include <hip/hip_runtime.h>
 #include "nw_point.h"
@@ -74,15 +74,36 @@ __global__ void __launch_bounds__(256) k_verify(VerifyParams a) {
     }
     a.flags[i] = flags;
     const ge_p3 P = compute_P<WA>(S, h, sok, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
-    store_xyz(a.pbuf + (size_t)i * PBUF_WORDS, P);
+    // P in processing order, struct-of-arrays (column gid): coalesced for k_finish
+    store_xyz_soa(a.pbuf, a.n, gid, P);
 }
 
 // ------------------------------------------------------------------------------------ signer grouping
 // Counting sort of signature indices by key-cache slot: perm lists the signatures of slot 0, then
 // slot 1, ...  (order inside a slot is arbitrary; every output is written at the original index).
+// Committees are small next to a batch (100 keys, 1M signatures), so global per-slot atomics would
+// serialize: each workgroup histograms a GROUP_TILE-signature tile in LDS and touches global
+// memory once per (tile, slot).  Above GROUP_LDS_KEYS slots the plain global-atomic form is used
+// (contention is then spread over many addresses anyway).
+static constexpr uint32_t GROUP_TILE = 4096;
+static constexpr uint32_t GROUP_LDS_KEYS = 8192;
+
 __global__ void __launch_bounds__(256) k_count_slots(uint32_t n, const uint32_t* signer, uint32_t* counts) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) atomicAdd(&counts[signer[i]], 1u);
+}
+
+__global__ void __launch_bounds__(256) k_count_slots_lds(uint32_t n, uint32_t nkeys, const uint32_t* signer,
+                                                         uint32_t* counts) {
+    extern __shared__ uint32_t hist[];
+    for (uint32_t k = threadIdx.x; k < nkeys; k += blockDim.x) hist[k] = 0;
+    __syncthreads();
+    const uint32_t t0 = blockIdx.x * GROUP_TILE;
+    const uint32_t t1 = min(n, t0 + GROUP_TILE);
+    for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&hist[signer[i]], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nkeys; k += blockDim.x)
+        if (hist[k]) atomicAdd(&counts[k], hist[k]);
 }
 
 // Single-block exclusive scan of counts[0..k) into cursor[0..k).
@@ -115,36 +136,64 @@ __global__ void __launch_bounds__(256) k_scatter_slots(uint32_t n, const uint32_
     if (i < n) perm[atomicAdd(&cursor[signer[i]], 1u)] = i;
 }
 
+// Tile-local scatter: LDS histogram -> one global atomic per (tile, slot) reserves the tile's run
+// of each slot -> LDS atomics rank the tile's signatures inside their runs.
+__global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t nkeys, const uint32_t* signer,
+                                                           uint32_t* cursor, uint32_t* perm) {
+    extern __shared__ uint32_t lds[];
+    uint32_t* base = lds;            // [nkeys] tile count, then the tile's global base
+    uint32_t* rank = lds + nkeys;    // [nkeys] running rank inside the tile
+    for (uint32_t k = threadIdx.x; k < nkeys; k += blockDim.x) {
+        base[k] = 0;
+        rank[k] = 0;
+    }
+    __syncthreads();
+    const uint32_t t0 = blockIdx.x * GROUP_TILE;
+    const uint32_t t1 = min(n, t0 + GROUP_TILE);
+    for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&base[signer[i]], 1u);
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nkeys; k += blockDim.x)
+        if (base[k]) base[k] = atomicAdd(&cursor[k], base[k]);
+    __syncthreads();
+    for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+        const uint32_t k = signer[i];
+        perm[base[k] + atomicAdd(&rank[k], 1u)] = i;
+    }
+}
+
 // ------------------------------------------------------------------------------------ finish
-// One lane per chunk of FINISH_K consecutive signatures: Montgomery batch inversion of their Z
-// (one field inversion per chunk), affine x, y, encoding match against R, strict verdict, and
-// (batch mode) compaction of the mismatching signatures into the exact-path list.
+// Montgomery batch inversion of the Z of FINISH_K signatures per lane (one field inversion per
+// chunk), affine x, y, encoding match against R, strict verdict, and (batch mode) compaction of the
+// mismatching signatures into the exact-path list.  Lane L of NL owns the processing-order columns
+// g = L, L + NL, L + 2 NL, ... so every pbuf / pre access of a wave is one contiguous 256-B run.
 __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
-    const uint64_t L = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t s0 = L * FINISH_K;
-    if (s0 >= a.n) return;
-    const uint32_t cnt = (uint32_t)((a.n - s0) < FINISH_K ? (a.n - s0) : FINISH_K);
+    const uint32_t NL = (a.n + FINISH_K - 1) / FINISH_K;
+    const uint32_t L = blockIdx.x * blockDim.x + threadIdx.x;
+    if (L >= NL) return;
+    const uint32_t cnt = (a.n - L + NL - 1) / NL;   // columns L + k NL < n
+    const size_t n = a.n;
     fe acc = fe_one();
     for (uint32_t k = 0; k < cnt; ++k) {
-        acc = fe_mul(acc, load_fe(a.pbuf + (s0 + k) * PBUF_WORDS + 20));
-        store_fe(a.pre + (s0 + k) * 10, acc);
+        const size_t g = L + (size_t)k * NL;
+        acc = fe_mul(acc, load_fe_soa(a.pbuf + 20 * n, n, g));
+        store_fe_soa(a.pre, n, g, acc);
     }
     fe inv = fe_invert(acc);
     for (int k = (int)cnt - 1; k >= 0; --k) {
-        const uint64_t i = s0 + k;
-        const uint32_t* pb = a.pbuf + i * PBUF_WORDS;
+        const size_t g = L + (size_t)k * NL;
         fe zi = inv;
         if (k > 0) {
-            zi = fe_mul(inv, load_fe(a.pre + (i - 1) * 10));
-            inv = fe_mul(inv, load_fe(pb + 20));
+            zi = fe_mul(inv, load_fe_soa(a.pre, n, g - NL));
+            inv = fe_mul(inv, load_fe_soa(a.pbuf + 20 * n, n, g));
         }
+        const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
         uint32_t R[8];
-        load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + i * 16);
-        uint32_t f = finish_flags(load_fe(pb), load_fe(pb + 10), zi, R, a.flags[i]);
+        load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
+        uint32_t f = finish_flags(load_fe_soa(a.pbuf, n, g), load_fe_soa(a.pbuf + 10 * n, n, g), zi, R, a.flags[i]);
         if (a.batch_mode && (f & (NW_F_S_OK | NW_F_A_OK)) == (NW_F_S_OK | NW_F_A_OK) && !(f & NW_F_MATCH)) {
             f |= NW_F_SLOW;
             const uint32_t t = atomicAdd(a.slow_count, 1u);
-            a.slow_list[t] = (uint32_t)i;
+            a.slow_list[t] = i;
             a.slow_slot[i] = t;
         }
         a.flags[i] = f;
@@ -365,9 +414,18 @@ hipError_t launch_group_by_signer(uint32_t n, uint32_t nkeys, const uint32_t* si
     if (n == 0 || nkeys == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(counts, 0, (size_t)nkeys * 4, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_count_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, signer, counts);
+    const bool lds = nkeys <= GROUP_LDS_KEYS;
+    if (lds)
+        hipLaunchKernelGGL(k_count_slots_lds, dim3(blocks_for(n, GROUP_TILE)), dim3(256), nkeys * 4, st, n, nkeys,
+                           signer, counts);
+    else
+        hipLaunchKernelGGL(k_count_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, signer, counts);
     hipLaunchKernelGGL(k_scan_slots, dim3(1), dim3(1024), 0, st, nkeys, counts, cursor);
-    hipLaunchKernelGGL(k_scatter_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, signer, cursor, perm);
+    if (lds)
+        hipLaunchKernelGGL(k_scatter_slots_lds, dim3(blocks_for(n, GROUP_TILE)), dim3(256), nkeys * 8, st, n, nkeys,
+                           signer, cursor, perm);
+    else
+        hipLaunchKernelGGL(k_scatter_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, signer, cursor, perm);
     return hipGetLastError();
 }
 

@@ -126,3 +126,20 @@ def worker_batch(n_tx: int, tx_size: int, batch_id: int = 0) -> bytes:
         parts.append(struct.pack("<Q", tx_size))
         parts.append(tx)
     return b"".join(parts)
+
+
+def worker_batches_np(n_batches: int, n_tx: int = 977, tx_size: int = 512) -> "np.ndarray":
+    """``n_batches`` serialized worker batches as one uint8[n_batches, 12 + n_tx * (8 + tx_size)]
+    array, byte-identical to ``worker_batch(n_tx, tx_size, b)`` for b = 0 .. n_batches - 1
+    (vectorized: the C4 node load is 10,000 x 508,052 B)."""
+    rec = 8 + tx_size
+    blen = 12 + n_tx * rec
+    out = np.zeros((n_batches, blen), np.uint8)
+    out[:, 4:12] = np.frombuffer(struct.pack("<Q", n_tx), np.uint8)
+    body = out[:, 12:].reshape(n_batches, n_tx, rec)
+    body[:, :, 0:8] = np.frombuffer(struct.pack("<Q", tx_size), np.uint8)
+    body[:, :, 8:12] = 0xFF
+    ctr = (np.arange(n_batches, dtype=np.uint64)[:, None] * n_tx + np.arange(n_tx, dtype=np.uint64)[None, :])
+    ctr = (ctr & 0xFFFFFFFF).astype(">u4")
+    body[:, :, 12:16] = ctr.view(np.uint8).reshape(n_batches, n_tx, 4)
+    return out
