@@ -1,8 +1,8 @@
 """narwhal_amd — MI355X-native Ed25519 verify + SHA-512 digest engine for Narwhal/Bullshark.
 
 Drop-in for the reference ``crypto`` crate's hot path:
-``narwhal_amd.crypto`` mirrors crypto/src/lib.rs; ``narwhal_amd.primary`` mirrors the
-certificate / header / vote callers; ``narwhal_amd.shard`` is the multi-GPU sharding layer.
+``narwhal_amd.crypto`` mirrors crypto/src/lib.rs; ``narwhal_amd.shard`` is the multi-GPU
+sharding layer; ``narwhal_amd.workload`` builds the synthetic committees and certificates.
 All compute runs in libnwcrypto.so (hand-written gfx950 HIP); importing without the built
 library raises ImportError.
 """
