@@ -31,7 +31,7 @@ METRIC = "Ed25519 sigs verified/s (node, 1/2/4/8 GPU); p50 latency per 2f+1 cert
 # kernel runs a different (cheaper) algorithm, so v1 is not its work.
 COST_MODEL_V1_FM = {3: 1750, 67: 1030, 667: 811, 977: 775, 6667: 644}
 MADS_PER_FM = 100          # 10 x 10 radix-2^25.5 limb products per field multiplication
-B_WINDOW = 16              # basepoint comb window (nw_point.h)
+B_WINDOW = 24              # basepoint comb window (nw_point.h)
 MADD_FM = 7                # mixed (affine Niels) addition = 7 field multiplications
 
 
@@ -175,6 +175,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-samples", type=int, default=200)
     ap.add_argument("--digest-batches", type=int, default=10000, help="0 disables the digest leg")
+    ap.add_argument("--key-window", type=int, default=-1,
+                    help="key comb window; -1 = committee mode (library sizes it for the loaded committee)")
     args = ap.parse_args()
 
     import numpy as np
@@ -189,7 +191,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from narwhal_amd import _lib, shard, workload
-    eng = _lib.Engine(device=local)
+    eng = _lib.Engine(device=local, key_window=args.key_window)
     com = workload.make_committee(args.validators, eng)
     slots = eng.committee_load_np(com.pks, com.stake)
     first_cert = rank * args.certs                      # each rank: its own shard of certificates

@@ -46,10 +46,14 @@ typedef struct nw_ctx nw_ctx;
 typedef struct nw_opts {
     int device;        /* HIP device ordinal (one process per GPU; -1 = current device) */
     uint32_t flags;    /* reserved, 0 */
-    size_t max_keys;   /* key-cache capacity in keys (0 = fill a 96 GiB HBM budget) */
-    int key_window;    /* key comb window: 8, 12 or 16 bits (0 = auto at the first load: 16 for
-                          <= 384 keys, 12 for <= 12288 keys, else 8).  Table bytes per key:
-                          w8 0.53 MB, w12 5.77 MB, w16 67.1 MB; additions per signature 32/22/16 */
+    size_t max_keys;   /* key-cache capacity in keys (0 = fill a 160 GiB HBM budget) */
+    int key_window;    /* key comb window: 8, 12, 16 or 20 bits.  0 = auto at the first load (16 for
+                          <= 384 keys, 12 for <= 12288 keys, else 8); -1 = committee mode: the first
+                          nw_committee_load is the committee, and the widest window whose tables
+                          fit the key budget with 25% headroom is used.  Table bytes per key:
+                          w8 0.53 MB, w12 5.77 MB, w16 67.1 MB, w20 872 MB; additions per signature
+                          32 / 22 / 16 / 13.  (The basepoint comb is fixed at w24: 11 additions,
+                          11.8 GB per context.) */
 } nw_opts;
 
 /* One certificate: its votes are sig[first_vote .. first_vote + n_votes). */
@@ -105,6 +109,17 @@ int nw_verify_batch(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len,
 int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint8_t (*sig)[64],
                     const uint32_t* signer_slot, const uint8_t (*msg)[32], const uint8_t zseed[32],
                     uint64_t cert_base, uint8_t* cert_ok, uint8_t* sig_ok, uint64_t* accepted_stake);
+
+/* Many independent dalek::verify_batch calls in one submission — the worker's simulated
+ * transaction-signature load (worker/src/processor.rs:75-79: 64 chunks per batch, 8-byte messages,
+ * keys fixed at spawn).  Batch b covers signatures [first[b], first[b] + n[b]); signature i signs
+ * msg[i] (len[i] bytes) under key-cache slot signer_slot[i] (nw_committee_load).  Outputs (each
+ * may be NULL): batch_ok[b] = 1 iff verify_batch of batch b is Ok (coefficients: NW-Z v1 with
+ * batch index batch_base + b); sig_ok[i] = verify_strict verdict of signature i. */
+int nw_verify_batches(nw_ctx* ctx, size_t nb, const uint32_t* first, const uint32_t* n,
+                      const uint8_t* const* msg, const size_t* len, const uint32_t* signer_slot,
+                      const uint8_t (*sig)[64], const uint8_t zseed[32], uint64_t batch_base, uint8_t* batch_ok,
+                      uint8_t* sig_ok);
 
 /* Device-resident variant for streaming use (inputs already in HBM).  All pointers are device
  * pointers; ``stream`` is a hipStream_t (NULL = default stream).  Enqueues work and returns;

@@ -50,6 +50,7 @@ def _load() -> ctypes.CDLL:
         "nw_verify_batch": (I, [P, P, P, P, P, S, P, U64]),
         "nw_verify_certs": (I, [P, P, S, P, P, P, P, U64, P, P, P]),
         "nw_verify_certs_dev": (I, [P, S, P, P, S, P, P, P, P, U64, P, P, P, P]),
+        "nw_verify_batches": (I, [P, S, P, P, P, P, P, P, P, U64, P, P]),
         "nw_sha512": (I, [P, P, S, P]),
         "nw_sha512_many": (I, [P, P, P, P, S, P]),
         "nw_sha512_many_dev": (I, [P, P, P, P, S, P, P]),
@@ -168,6 +169,42 @@ class Engine:
         self.check(LIB.nw_verify_certs(self._ctx, certs, nc, _buf(sigs_blob), slots, _buf(msgs_blob), bytes(zseed),
                                        cert_base, cert_ok, sig_ok, stake), "nw_verify_certs")
         return [bool(x) for x in cert_ok[:nc]], [bool(x) for x in sig_ok[:nsig]], list(stake[:nc])
+
+    def verify_batches(self, batches, msgs, signer_slots, sigs, zseed: bytes, batch_base: int = 0):
+        """batches: list of (first, n); msgs: per-signature bytes; signer_slots: key-cache slots;
+        sigs: per-signature 64-byte signatures.  Returns (batch_ok list, sig_ok list)."""
+        nb, ns = len(batches), len(sigs)
+        first = (ctypes.c_uint32 * max(nb, 1))(*[f for f, _ in batches])
+        cnt = (ctypes.c_uint32 * max(nb, 1))(*[n for _, n in batches])
+        mp = (ctypes.c_char_p * max(ns, 1))(*[bytes(m) for m in msgs])
+        ln = (ctypes.c_size_t * max(ns, 1))(*[len(m) for m in msgs])
+        slots = (ctypes.c_uint32 * max(ns, 1))(*signer_slots)
+        bok = (ctypes.c_uint8 * max(nb, 1))()
+        sok = (ctypes.c_uint8 * max(ns, 1))()
+        self.check(LIB.nw_verify_batches(self._ctx, nb, first, cnt, mp, ln, slots,
+                                         _buf(b"".join(map(bytes, sigs))), bytes(zseed), batch_base, bok, sok),
+                   "nw_verify_batches")
+        return [bool(x) for x in bok[:nb]], [bool(x) for x in sok[:ns]]
+
+    def verify_batches_np(self, first, counts, msgs, signer_slots, sigs, zseed: bytes, batch_base: int = 0):
+        """numpy variant: msgs uint8[N, L] (fixed-length messages, e.g. the worker's 8-byte ones),
+        sigs uint8[N, 64], signer_slots uint32[N].  Returns (batch_ok u8[B], sig_ok u8[N])."""
+        import numpy as np
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        sigs = np.ascontiguousarray(sigs, dtype=np.uint8)
+        slots = np.ascontiguousarray(signer_slots, dtype=np.uint32)
+        first = np.ascontiguousarray(first, dtype=np.uint32)
+        counts = np.ascontiguousarray(counts, dtype=np.uint32)
+        n, ml = msgs.shape
+        ptrs = (msgs.ctypes.data + np.arange(n, dtype=np.uint64) * ml).astype(np.uint64)
+        lens = np.full(n, ml, dtype=np.uint64)
+        bok = np.zeros(max(len(first), 1), np.uint8)
+        sok = np.zeros(max(n, 1), np.uint8)
+        self.check(LIB.nw_verify_batches(self._ctx, len(first), first.ctypes.data, counts.ctypes.data,
+                                         ptrs.ctypes.data, lens.ctypes.data, slots.ctypes.data, sigs.ctypes.data,
+                                         bytes(zseed), batch_base, bok.ctypes.data, sok.ctypes.data),
+                   "nw_verify_batches")
+        return bok[:len(first)], sok[:n]
 
     # -- digests ------------------------------------------------------------------------------
     def sha512(self, data: bytes) -> bytes:

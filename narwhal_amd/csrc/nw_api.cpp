@@ -93,10 +93,23 @@ const uint8_t kBaseEnc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x
                               0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                               0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
 
-constexpr size_t KEY_CACHE_BUDGET = 96ull << 30;   // bytes of HBM for key tables by default
+constexpr size_t KEY_CACHE_BUDGET = 160ull << 30;  // bytes of HBM for key tables by default (of 288 GB)
 constexpr size_t kGroupMinSigs = 16384;            // group signatures by signer above this batch size
 
+// Key comb window, fixed at the first load.  Auto (0): a conservative choice that leaves room for
+// keys added later.  Committee mode (-1): the first load IS the committee; take the widest window
+// whose tables for it fit the key budget with 25% headroom (fewest additions per signature).
+int committee_window(size_t n, size_t budget) {
+    for (int w : {20, 16, 12}) {
+        const double need = 1.25 * (double)n * (double)comb_words(w) * 4.0;
+        if (need <= (double)budget) return w;
+    }
+    return 8;
+}
+
 void fix_window(nw_ctx* ctx, size_t first_load) {
+    const size_t budget = ctx->max_keys_user ? (size_t)-1 : KEY_CACHE_BUDGET;
+    if (ctx->key_window == -1) ctx->key_window = committee_window(first_load, budget);
     if (ctx->key_window == 0) ctx->key_window = first_load <= 384 ? 16 : (first_load <= 12288 ? 12 : 8);
     ctx->key_words = comb_words(ctx->key_window);
     if (!ctx->max_keys_user) ctx->max_keys = KEY_CACHE_BUDGET / (ctx->key_words * 4);
@@ -139,14 +152,15 @@ int grow_keys(nw_ctx* ctx, size_t need) {
 
 // Build tables for keys [k0, k0 + nk) whose raw bytes are already in d_keys_raw.
 int build_keys(nw_ctx* ctx, uint32_t* d_raw, uint32_t* d_info, uint32_t* d_tab, size_t nk, int window) {
-    const size_t chunk = window == 16 ? 64 : 4096;   // bounds the bases scratch and grid size
+    // keys per launch: bounds the bases scratch and keeps a launch near 16M chunk threads
+    const size_t chunk = window >= 24 ? 1 : (window == 20 ? 16 : (window == 16 ? 256 : 4096));
     const size_t words = comb_words(window);
     for (size_t s = 0; s < nk; s += chunk) {
         const size_t m = nk - s < chunk ? nk - s : chunk;
         NW_TRY(ctx->w_bases.ensure(m * comb_pos(window) * 40 * 4), "hipMalloc(bases)");
         NW_TRY(launch_key_prep((uint32_t)m, d_raw + s * 8, d_info + s, ctx->w_bases.as<uint32_t>(), d_tab + s * words,
                                window, ctx->stream),
-               "k_key_prep/k_comb_entries");
+               "k_key_prep/k_comb_build");
     }
     return NW_OK;
 }
@@ -179,7 +193,7 @@ int ensure_slots(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, si
         ctx->h_stake.push_back(stake ? stake[i] : 0u);
     }
     const size_t add = pending.size();
-    if (add && ctx->key_window == 0) fix_window(ctx, add);
+    if (add && ctx->key_window <= 0) fix_window(ctx, add);
     if (add) {
         int rc = grow_keys(ctx, ctx->nkeys + add);
         if (rc != NW_OK) {
@@ -392,12 +406,13 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
         ctx->max_keys_user = true;
     }
     if (opts && opts->key_window) {
-        if (opts->key_window != 8 && opts->key_window != 12 && opts->key_window != 16) {
+        if (opts->key_window != -1 && opts->key_window != 8 && opts->key_window != 12 && opts->key_window != 16 &&
+            opts->key_window != 20) {
             delete ctx;
             return NW_ERR_ARG;
         }
         ctx->key_window = opts->key_window;
-        fix_window(ctx, 0);
+        if (ctx->key_window > 0) fix_window(ctx, 0);
     }
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
@@ -567,6 +582,56 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
     if (cert_ok && ncerts) NW_TRY(hipMemcpyAsync(cert_ok, ctx->w_cert_ok.p, ncerts, hipMemcpyDeviceToHost, st), "D2H");
     if (accepted_stake && ncerts)
         NW_TRY(hipMemcpyAsync(accepted_stake, ctx->w_stake_out.p, ncerts * 8, hipMemcpyDeviceToHost, st), "D2H");
+    NW_TRY(hipStreamSynchronize(st), "sync");
+    return NW_OK;
+}
+
+int nw_verify_batches(nw_ctx* ctx, size_t nb, const uint32_t* first, const uint32_t* nvotes,
+                      const uint8_t* const* msg, const size_t* len, const uint32_t* signer_slot,
+                      const uint8_t (*sig)[64], const uint8_t zseed[32], uint64_t batch_base, uint8_t* batch_ok,
+                      uint8_t* sig_ok) {
+    if (!ctx || (nb && (!first || !nvotes))) return NW_ERR_ARG;
+    std::lock_guard<std::mutex> g(ctx->mu);
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    size_t nsigs = 0;
+    for (size_t b = 0; b < nb; ++b) {
+        const size_t end = (size_t)first[b] + nvotes[b];
+        if (end > nsigs) nsigs = end;
+    }
+    if (nsigs && (!sig || !signer_slot || !msg || !len)) return NW_ERR_ARG;
+    for (size_t v = 0; v < nsigs; ++v)
+        if (signer_slot[v] >= ctx->nkeys) {
+            ctx->last_error = "signer slot out of range (load the keys first)";
+            return NW_ERR_ARG;
+        }
+    hipStream_t st = ctx->stream;
+    int rc = upload_messages(ctx, msg, len, nsigs);
+    if (rc != NW_OK) return rc;
+    NW_TRY(ctx->w_sig.ensure(nsigs * 64 + 64), "ws sig");
+    NW_TRY(ctx->w_signer.ensure(nsigs * 4 + 4), "ws signer");
+    NW_TRY(ctx->w_cert_first.ensure(nb * 4 + 4), "ws first");
+    NW_TRY(ctx->w_cert_n.ensure(nb * 4 + 4), "ws n");
+    NW_TRY(ctx->w_cert_ok.ensure(nb + 16), "ws batch_ok");
+    NW_TRY(ctx->w_ok.ensure(nsigs + 16), "ws ok");
+    if (nsigs) {
+        NW_TRY(hipMemcpyAsync(ctx->w_sig.p, sig, nsigs * 64, hipMemcpyHostToDevice, st), "H2D sig");
+        NW_TRY(hipMemcpyAsync(ctx->w_signer.p, signer_slot, nsigs * 4, hipMemcpyHostToDevice, st), "H2D signer");
+    }
+    if (nb) {
+        NW_TRY(hipMemcpyAsync(ctx->w_cert_first.p, first, nb * 4, hipMemcpyHostToDevice, st), "H2D first");
+        NW_TRY(hipMemcpyAsync(ctx->w_cert_n.p, nvotes, nb * 4, hipMemcpyHostToDevice, st), "H2D n");
+    }
+    rc = enqueue_certs(ctx, nb, ctx->w_cert_first.as<uint32_t>(), ctx->w_cert_n.as<uint32_t>(), nsigs,
+                       ctx->w_sig.as<uint8_t>(), ctx->w_signer.as<uint32_t>(), 1, nullptr, ctx->w_msg.as<uint8_t>(),
+                       ctx->w_msg_off.as<uint64_t>(), ctx->w_msg_len.as<uint64_t>(), zseed, batch_base, 1,
+                       ctx->w_cert_ok.as<uint8_t>(), nullptr, nullptr, st);
+    if (rc != NW_OK) return rc;
+    if (sig_ok && nsigs) {
+        NW_TRY(launch_flags_to_ok((uint32_t)nsigs, ctx->w_flags.as<uint32_t>(), ctx->w_ok.as<uint8_t>(), st),
+               "k_flags_to_ok");
+        NW_TRY(hipMemcpyAsync(sig_ok, ctx->w_ok.p, nsigs, hipMemcpyDeviceToHost, st), "D2H sig_ok");
+    }
+    if (batch_ok && nb) NW_TRY(hipMemcpyAsync(batch_ok, ctx->w_cert_ok.p, nb, hipMemcpyDeviceToHost, st), "D2H");
     NW_TRY(hipStreamSynchronize(st), "sync");
     return NW_OK;
 }

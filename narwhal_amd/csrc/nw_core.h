@@ -96,9 +96,10 @@ NW_HD void hram_generic(uint32_t out[16], const uint32_t R[8], const uint32_t A[
 
 // One comb pass: P += sum_pos sign(d_pos) * T[pos][|d_pos|] for the signed radix-2^W digits of
 // sc (consumed).  Software-pipelined: the gather of position pos+1's entry is issued before the
-// mixed addition of position pos, so the (HBM / Infinity-Cache) latency hides under ~1.3k VALU
-// instructions of field arithmetic.  neg_pos: negate entries for positive digits (-h A).
-template <int W>
+// mixed addition of position pos, so the (HBM) latency hides under ~1.3k VALU instructions of
+// field arithmetic.  neg_pos: negate entries for positive digits (-h A).  FIRST: P is the identity
+// on entry, so position 0's entry becomes P directly (ge_from_precomp: 1 multiplication, not 7).
+template <int W, bool FIRST>
 NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab, bool neg_pos) {
     int carry = 0;
     int d = next_digit<W>(sc, carry);
@@ -106,8 +107,39 @@ NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab,
     uint4 cur[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) cur[k] = q[k];
+    int pos = 0;
+    if constexpr (FIRST) {
+        // position 0 starts the chain: P = T[0][|d|] (sign applied), no addition
+        uint32_t w[32];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            w[4 * k] = cur[k].x;
+            w[4 * k + 1] = cur[k].y;
+            w[4 * k + 2] = cur[k].z;
+            w[4 * k + 3] = cur[k].w;
+        }
+        const bool neg0 = neg_pos ? d > 0 : d < 0;
+        d = next_digit<W>(sc, carry);   // position 1's digit; its gather overlaps the conversion
+        const uint4* qn = reinterpret_cast<const uint4*>(tab + ((size_t)comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) cur[k] = qn[k];
+        P = ge_from_precomp(ge_precomp_cneg(ge_precomp_from_words(w), neg0));
+        pos = 1;
+    }
 #pragma nounroll
-    for (int pos = 0; pos < comb_pos(W); ++pos) {
+    for (; pos < comb_pos(W); ++pos) {
+#ifdef NW_NO_PREFETCH
+        uint4 nxt[8];
+        int dn = 0;
+        uint32_t w[32];
+        {
+            const uint4* qc = reinterpret_cast<const uint4*>(
+                tab + ((size_t)pos * comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) cur[k] = qc[k];
+        }
+        if (pos + 1 < comb_pos(W)) dn = next_digit<W>(sc, carry);
+#else
         uint4 nxt[8];
         int dn = 0;
         if (pos + 1 < comb_pos(W)) {
@@ -118,6 +150,7 @@ NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab,
             for (int k = 0; k < 8; ++k) nxt[k] = qn[k];
         }
         uint32_t w[32];
+#endif
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             w[4 * k] = cur[k].x;
@@ -126,8 +159,10 @@ NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab,
             w[4 * k + 3] = cur[k].w;
         }
         P = ge_madd(P, ge_precomp_cneg(ge_precomp_from_words(w), neg_pos ? d > 0 : d < 0));
+#ifndef NW_NO_PREFETCH
 #pragma unroll
         for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
+#endif
         d = dn;
     }
 }
@@ -143,9 +178,9 @@ NW_HD ge_p3 comb_sB_minus_hA(const uint32_t s_in[8], const uint32_t h_in[8], con
         s[k] = s_in[k];
         h[k] = h_in[k];
     }
-    ge_p3 P = ge_identity();
-    comb_pass<WB>(P, s, btab, false);
-    if constexpr (WA > 0) comb_pass<WA>(P, h, atab, true);
+    ge_p3 P;
+    comb_pass<WB, true>(P, s, btab, false);
+    if constexpr (WA > 0) comb_pass<WA, false>(P, h, atab, true);
     return P;
 }
 
@@ -164,13 +199,13 @@ NW_HD void hram_msg32(uint32_t h[8], const uint32_t R[8], const uint32_t A[8], c
 }
 
 // P = s B - h A (s forced to 0 when non-canonical so the comb's digit range stays valid).
-template <int WA>
+template <int WA, int WB = B_WINDOW>
 NW_HD ge_p3 compute_P(const uint32_t S[8], const uint32_t h[8], bool sok, const uint32_t* btab,
                       const uint32_t* atab) {
     uint32_t s_use[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) s_use[k] = sok ? S[k] : 0u;
-    return comb_sB_minus_hA<B_WINDOW, WA>(s_use, h, btab, atab);
+    return comb_sB_minus_hA<WB, WA>(s_use, h, btab, atab);
 }
 
 NW_HD fe load_fe(const uint32_t* p) {
@@ -321,8 +356,69 @@ NW_HD void comb_entry_one(const uint32_t* bases, uint32_t pos, uint32_t e, uint3
     dst[31] = 0;
 }
 
+// Comb-table builder for entries [CH c, CH c + CH) of one (key, position): consecutive multiples
+// Q_k = (CH c + k) * base by repeated addition, then ONE field inversion for the whole chunk
+// (Montgomery's trick, prefix products kept in registers) to reach affine Niels form.  The chunk's
+// projective X, Y, Z are parked in their own table slots between the two passes.  About 90 field
+// multiplications per entry instead of ~500 for a per-entry double-and-add plus inversion.
+template <int W, int CH>
+NW_HD void comb_chunk_build(const uint32_t* bases, uint32_t pos, uint32_t c, uint32_t* tab) {
+    constexpr uint32_t ENT = (uint32_t)comb_ent(W);
+    constexpr int NB = 32 - __builtin_clz((ENT - 1) / CH);   // bits of the largest chunk index
+    const uint32_t e0 = c * CH;
+    const uint32_t cnt = ENT - e0 < (uint32_t)CH ? ENT - e0 : (uint32_t)CH;
+    const ge_p3 base = load_p3(bases + (size_t)pos * 40);
+    const ge_cached bc = ge_to_cached(base);
+    ge_p3 stride = base;
+#pragma unroll
+    for (int k = 1; k < CH; k <<= 1) stride = ge_dbl(stride);
+    const ge_cached sc = ge_to_cached(stride);
+    ge_p3 Q = ge_identity();   // Q = c * stride, uniform double-and-add over NB bits
+#pragma nounroll
+    for (int b = NB - 1; b >= 0; --b) {
+        Q = ge_dbl(Q);
+        const ge_p3 Qa = ge_add(Q, sc);
+        Q = ge_select(Q, Qa, ((c >> b) & 1u) != 0);
+    }
+    uint32_t* slot0 = tab + ((size_t)pos * ENT + e0) * PRECOMP_WORDS;
+    fe pre[CH];
+    fe acc = fe_one();
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+        if ((uint32_t)k < cnt) {
+            uint32_t* sl = slot0 + (size_t)k * PRECOMP_WORDS;
+            store_fe(sl, Q.X);
+            store_fe(sl + 10, Q.Y);
+            store_fe(sl + 20, Q.Z);
+            acc = fe_mul(acc, Q.Z);
+            pre[k] = acc;
+            if ((uint32_t)k + 1 < cnt) Q = ge_add(Q, bc);
+        }
+    }
+    fe inv = fe_invert(acc);
+#pragma unroll
+    for (int k = CH - 1; k >= 0; --k) {
+        if ((uint32_t)k < cnt) {
+            uint32_t* sl = slot0 + (size_t)k * PRECOMP_WORDS;
+            const fe Z = load_fe(sl + 20);
+            fe zi = inv;
+            if (k > 0) {
+                zi = fe_mul(inv, pre[k - 1]);
+                inv = fe_mul(inv, Z);
+            }
+            const fe x = fe_mul(load_fe(sl), zi);
+            const fe y = fe_mul(load_fe(sl + 10), zi);
+            store_fe(sl, fe_carry(fe_add(y, x)));
+            store_fe(sl + 10, fe_sub(y, x));
+            store_fe(sl + 20, fe_mul(fe_mul(x, y), fe_from_const(FE_D2)));
+            sl[30] = 0;
+            sl[31] = 0;
+        }
+    }
+}
+
 // RFC 8032 Ed25519 signing of an MW-word message (crypto::Signature::new, crypto/src/lib.rs:185-191).
-template <int MW>
+template <int MW, int WB = B_WINDOW>
 NW_HD void sign_one(const uint32_t* seed_in, const uint32_t* msg_in, const uint32_t* btab, uint32_t pk[8],
                     uint32_t sig[16]) {
     uint32_t seed[8], m[MW];
@@ -345,7 +441,7 @@ NW_HD void sign_one(const uint32_t* seed_in, const uint32_t* msg_in, const uint3
     sc_reduce512(ared, wide);
     uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t Aw[8];
-    ge_compress_w(Aw, comb_sB_minus_hA<B_WINDOW, 0>(ared, zero8, btab, nullptr));
+    ge_compress_w(Aw, comb_sB_minus_hA<WB, 0>(ared, zero8, btab, nullptr));
     uint32_t pm[8 + MW];
 #pragma unroll
     for (int k = 0; k < 8; ++k) pm[k] = hs[8 + k];
@@ -356,7 +452,7 @@ NW_HD void sign_one(const uint32_t* seed_in, const uint32_t* msg_in, const uint3
     uint32_t r[8];
     sc_reduce512(r, rh);
     uint32_t Rw[8];
-    ge_compress_w(Rw, comb_sB_minus_hA<B_WINDOW, 0>(r, zero8, btab, nullptr));
+    ge_compress_w(Rw, comb_sB_minus_hA<WB, 0>(r, zero8, btab, nullptr));
     uint32_t ram[16 + MW];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {

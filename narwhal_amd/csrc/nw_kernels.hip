@@ -282,16 +282,20 @@ __global__ void __launch_bounds__(64) k_key_prep(uint32_t nk, const uint32_t* ke
     key_info[j] = key_prep_one<W>(keys_raw + (size_t)j * 8, bases + (size_t)j * comb_pos(W) * 40);
 }
 
-// One thread per (key, position, entry): entry e of position pos = e * 2^(W pos) * A, affine Niels.
+// One thread per (key, position, chunk of COMB_CH entries): consecutive multiples with one batched
+// inversion per chunk (comb_chunk_build).
+static constexpr int COMB_CH = 8;
+
 template <int W>
-__global__ void __launch_bounds__(256) k_comb_entries(uint32_t nk, const uint32_t* bases, uint32_t* tab) {
+__global__ void __launch_bounds__(256) k_comb_build(uint32_t nk, const uint32_t* bases, uint32_t* tab) {
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t per_key = (uint64_t)comb_pos(W) * comb_ent(W);
+    const uint64_t nch = (comb_ent(W) + COMB_CH - 1) / COMB_CH;
+    const uint64_t per_key = (uint64_t)comb_pos(W) * nch;
     if (gid >= (uint64_t)nk * per_key) return;
     const uint32_t j = (uint32_t)(gid / per_key);
-    const uint32_t rem = (uint32_t)(gid % per_key);
-    comb_entry_one<W>(bases + (size_t)j * comb_pos(W) * 40, rem / comb_ent(W), rem % comb_ent(W),
-                      tab + (size_t)j * comb_words(W));
+    const uint64_t rem = gid % per_key;
+    comb_chunk_build<W, COMB_CH>(bases + (size_t)j * comb_pos(W) * 40, (uint32_t)(rem / nch), (uint32_t)(rem % nch),
+                                 tab + (size_t)j * comb_words(W));
 }
 
 // ------------------------------------------------------------------------------------ SHA-512 bulk
@@ -387,16 +391,20 @@ static void launch_verify_w(const VerifyParams& p, int wa, bool slow, uint32_t n
             if (slow) hipLaunchKernelGGL((k_slow_sig<MSGMODE, 12>), g, b, 0, st, p);
             else hipLaunchKernelGGL((k_verify<MSGMODE, 12>), g, b, 0, st, p);
             break;
-        default:
+        case 16:
             if (slow) hipLaunchKernelGGL((k_slow_sig<MSGMODE, 16>), g, b, 0, st, p);
             else hipLaunchKernelGGL((k_verify<MSGMODE, 16>), g, b, 0, st, p);
+            break;
+        default:
+            if (slow) hipLaunchKernelGGL((k_slow_sig<MSGMODE, 20>), g, b, 0, st, p);
+            else hipLaunchKernelGGL((k_verify<MSGMODE, 20>), g, b, 0, st, p);
             break;
     }
 }
 
 static hipError_t launch_vs(const VerifyParams& p, int msgmode, int key_window, bool slow, uint32_t n_upper,
                             hipStream_t st) {
-    if (key_window != 8 && key_window != 12 && key_window != 16) return hipErrorInvalidValue;
+    if (key_window != 8 && key_window != 12 && key_window != 16 && key_window != 20) return hipErrorInvalidValue;
     if (msgmode == 0)
         launch_verify_w<0>(p, key_window, slow, n_upper, st);
     else
@@ -467,8 +475,8 @@ static hipError_t launch_key_prep_w(uint32_t nk, const uint32_t* keys_raw, uint3
     hipLaunchKernelGGL(k_key_prep<W>, dim3(blocks_for(nk, 64)), dim3(64), 0, st, nk, keys_raw, key_info, bases);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const uint64_t total = (uint64_t)nk * comb_pos(W) * comb_ent(W);
-    hipLaunchKernelGGL(k_comb_entries<W>, dim3(blocks_for(total, 256)), dim3(256), 0, st, nk, bases, tab);
+    const uint64_t total = (uint64_t)nk * comb_pos(W) * ((comb_ent(W) + COMB_CH - 1) / COMB_CH);
+    hipLaunchKernelGGL(k_comb_build<W>, dim3(blocks_for(total, 256)), dim3(256), 0, st, nk, bases, tab);
     return hipGetLastError();
 }
 
@@ -479,6 +487,8 @@ hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_
         case 8: return launch_key_prep_w<8>(nk, keys_raw, key_info, bases, tab, st);
         case 12: return launch_key_prep_w<12>(nk, keys_raw, key_info, bases, tab, st);
         case 16: return launch_key_prep_w<16>(nk, keys_raw, key_info, bases, tab, st);
+        case 20: return launch_key_prep_w<20>(nk, keys_raw, key_info, bases, tab, st);
+        case B_WINDOW: return launch_key_prep_w<B_WINDOW>(nk, keys_raw, key_info, bases, tab, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -26,13 +26,14 @@ struct ge_cached {
 //   [0..9] y+x, [10..19] y-x, [20..29] 2dxy, [30..31] zero pad.
 static constexpr int PRECOMP_WORDS = 32;
 // Fixed-base combs: signed radix-2^W digits, one table per digit position holding the multiples
-// |d| * 2^(W*pos) * P for |d| = 0..2^(W-1) (0 = identity).  W = 16 for the basepoint (67 MB,
-// shared by every signature); W = 8 / 12 / 16 for committee keys, chosen by committee size so the
-// key cache fits HBM (nw_opts.key_window).  Additions per scalar = ceil(256 / W); no doublings.
+// |d| * 2^(W*pos) * P for |d| = 0..2^(W-1) (0 = identity).  W = 24 for the basepoint (11 positions,
+// 11.8 GB, shared by every signature: HBM-resident by design, 288 GB per GPU); W = 8 / 12 / 16 / 20
+// for committee keys, chosen by committee size so the key cache fits its HBM budget
+// (nw_opts.key_window).  Additions per scalar = ceil(256 / W); no doublings.
 NW_HD constexpr int comb_pos(int w) { return (256 + w - 1) / w; }
 NW_HD constexpr int comb_ent(int w) { return (1 << (w - 1)) + 1; }
 NW_HD constexpr size_t comb_words(int w) { return (size_t)comb_pos(w) * comb_ent(w) * PRECOMP_WORDS; }
-static constexpr int B_WINDOW = 16;
+static constexpr int B_WINDOW = 24;
 
 NW_HD ge_p3 ge_identity() {
     ge_p3 r;
@@ -66,6 +67,19 @@ NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) {
     r.Y = fe_mul(g, h);
     r.Z = fe_mul(g, f);
     r.T = fe_mul(e, h);
+    return r;
+}
+
+// Extended point of an affine Niels entry, with no field multiplication beyond T:
+// X = (y+x) - (y-x) = 2x, Y = (y+x) + (y-x) = 2y, Z = 2, T = 2xy = (2dxy) / d.
+// Starts a comb chain without the 7-multiplication addition to the identity.
+NW_HD ge_p3 ge_from_precomp(const ge_precomp& q) {
+    ge_p3 r;
+    r.X = fe_sub(q.ypx, q.ymx);
+    r.Y = fe_carry(fe_add(q.ypx, q.ymx));
+    r.Z = fe_zero();
+    r.Z.v[0] = 2;
+    r.T = fe_mul(q.xy2d, fe_from_const(FE_INVD));
     return r;
 }
 

@@ -679,11 +679,37 @@ int nwr_verify_strict(const uint8_t* msg, size_t len, const uint8_t pk[32], cons
     return ge_eq(&Rp, &R);
 }
 
+/* dalek::verify_batch core: signature i over msgs[i] (lens[i] bytes).  Key decompression per
+ * call (crypto/src/lib.rs:216 for certificates; dalek PublicKey values for the worker). */
+static int verify_batch_core(const uint8_t* const* msgs, const size_t* lens, const uint8_t (*pk)[32],
+                             const uint8_t (*sig)[64], size_t n, const uint8_t zseed[32], uint64_t bidx);
+
 /* crypto::Signature::verify_batch over one certificate: votes (pk_i, sig_i) all over msg.
  * Per-vote key decompression as crypto/src/lib.rs:216.  Returns 1 (Ok) / 0 (Err). */
 int nwr_crypto_verify_batch(const uint8_t* msg, size_t len, const uint8_t (*pk)[32], const uint8_t (*sig)[64],
                             size_t n, const uint8_t zseed[32], uint64_t bidx) {
     nwr_init();
+    const uint8_t** msgs = (const uint8_t**)malloc(sizeof(uint8_t*) * (n ? n : 1));
+    size_t* lens = (size_t*)malloc(sizeof(size_t) * (n ? n : 1));
+    for (size_t i = 0; i < n; ++i) {
+        msgs[i] = msg;
+        lens[i] = len;
+    }
+    const int ok = verify_batch_core(msgs, lens, pk, sig, n, zseed, bidx);
+    free(msgs);
+    free(lens);
+    return ok;
+}
+
+/* ed25519_dalek::verify_batch with per-signature messages (worker/src/processor.rs:78). */
+int nwr_verify_batch_msgs(const uint8_t* const* msgs, const size_t* lens, const uint8_t (*pk)[32],
+                          const uint8_t (*sig)[64], size_t n, const uint8_t zseed[32], uint64_t bidx) {
+    nwr_init();
+    return verify_batch_core(msgs, lens, pk, sig, n, zseed, bidx);
+}
+
+static int verify_batch_core(const uint8_t* const* msgs, const size_t* lens, const uint8_t (*pk)[32],
+                             const uint8_t (*sig)[64], size_t n, const uint8_t zseed[32], uint64_t bidx) {
     for (size_t i = 0; i < n; ++i)
         if (sig[i][63] & 0xE0) return 0;
     const size_t npts = 2 * n + 1;
@@ -697,7 +723,7 @@ int nwr_crypto_verify_batch(const uint8_t* msg, size_t len, const uint8_t (*pk)[
     uint8_t bsum[32] = {0};
     for (size_t i = 0; i < n && ok; ++i) {
         uint8_t h[64], hr[32], z[32], zs[32];
-        sha512_3(h, sig[i], 32, pk[i], 32, msg, len);
+        sha512_3(h, sig[i], 32, pk[i], 32, msgs[i], lens[i]);
         sc_from_hash(hr, h);
         nwz(z, zseed, (uint32_t)i, bidx);
         sc_mul(zs, z, sig[i] + 32);

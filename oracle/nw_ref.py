@@ -15,6 +15,7 @@ _lib.nwr_verify_strict.argtypes = [_P, _S, _P, _P]
 _lib.nwr_crypto_verify_batch.argtypes = [_P, _S, _P, _P, _S, _P, ctypes.c_uint64]
 _lib.nwr_decompress.argtypes = [_P, _P]
 _lib.nwr_sha512.argtypes = [_P, _S, _P]
+_lib.nwr_verify_batch_msgs.argtypes = [_P, _P, _P, _P, _S, _P, ctypes.c_uint64]
 _lib.nwr_verify_certs.argtypes = [_P, _P, _P, _P, _P, _P, _P, _S, _P, ctypes.c_uint64, ctypes.c_int, _P]
 _lib.nwr_init()
 
@@ -28,6 +29,15 @@ def crypto_verify_batch(digest: bytes, votes, zseed: bytes, batch_index: int = 0
     pks = b"".join(k for k, _ in votes)
     sigs = b"".join(s for _, s in votes)
     return bool(_lib.nwr_crypto_verify_batch(digest, len(digest), pks or None, sigs or None, n, zseed, batch_index))
+
+
+def verify_batch_msgs(msgs, pks, sigs, zseed: bytes, batch_index: int = 0) -> bool:
+    """dalek::verify_batch with per-signature messages (worker/src/processor.rs:78)."""
+    n = len(sigs)
+    mp = (ctypes.c_char_p * max(n, 1))(*[bytes(m) for m in msgs])
+    ln = (ctypes.c_size_t * max(n, 1))(*[len(m) for m in msgs])
+    return bool(_lib.nwr_verify_batch_msgs(mp, ln, b"".join(pks) or None, b"".join(sigs) or None, n, zseed,
+                                           batch_index))
 
 
 def decompress(b: bytes):

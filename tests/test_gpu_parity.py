@@ -301,3 +301,37 @@ def test_key_windows_adversarial(window, golden):
             bad.append(c["name"])
     assert not bad
     eng.close()
+
+
+# ----------------------------------------------------------------------------- worker load (A13)
+def test_verify_batches_worker_chunks(engine):
+    """worker/src/processor.rs:75-79: fixed keypairs, 8-byte LE messages i, the batch split into
+    64 chunks [count*c/64, min(count, count*(c+1)/64)), one dalek::verify_batch per chunk — here one
+    nw_verify_batches call.  Some chunks carry a bad signature (wrong message / bit flip / S >= l);
+    every chunk verdict and per-signature verdict is checked against the oracle."""
+    rng = random.Random(21)
+    count = 300
+    seeds = [bytes(rng.randrange(256) for _ in range(32)) for _ in range(count)]
+    msgs = [struct_le(i) for i in range(count)]
+    pks, sigs = engine.sign_many(seeds, msgs)
+    slots = engine.committee_load(pks)
+    bad = {7: "flip", 100: "msg", 201: "s_ge_l"}
+    for i, how in bad.items():
+        s = bytearray(sigs[i])
+        if how == "flip":
+            s[3] ^= 0x10
+        elif how == "msg":
+            s = bytearray(o.sign(seeds[i], b"other"))
+        else:
+            sv = int.from_bytes(s[32:], "little") + o.L
+            s[32:] = sv.to_bytes(32, "little")
+        sigs[i] = bytes(s)
+    chunks = [((count * c) // 64, min(count, (count * (c + 1)) // 64) - (count * c) // 64) for c in range(64)]
+    zseed = bytes(rng.randrange(256) for _ in range(32))
+    batch_ok, sig_ok = engine.verify_batches(chunks, msgs, slots, sigs, zseed, 1000)
+    for c, (f, n) in enumerate(chunks):
+        zs = o.batch_coefficients(zseed, 1000 + c, n)
+        want = o.verify_batch_z(msgs[f:f + n], sigs[f:f + n], pks[f:f + n], zs)
+        assert batch_ok[c] == want, c
+        assert want == all(i not in bad for i in range(f, f + n))
+    assert sig_ok == [o.verify_strict(pks[i], msgs[i], sigs[i]) for i in range(count)]

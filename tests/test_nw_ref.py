@@ -74,3 +74,20 @@ def test_torsion_batch_agrees_with_oracle():
         zs = o.batch_coefficients(bytes(32), bidx, len(votes))
         want = o.verify_batch_z([msg] * len(votes), [s for _, s in votes], [k for k, _ in votes], zs)
         assert nw_ref.crypto_verify_batch(msg, votes, bytes(32), bidx) == want == (zs[-1] % 2 == 0)
+
+
+def test_verify_batch_msgs_matches_oracle():
+    """Per-signature-message batches (worker/src/processor.rs:78) agree with the Python oracle."""
+    import random
+    rng = random.Random(9)
+    seeds = [bytes(rng.randrange(256) for _ in range(32)) for _ in range(6)]
+    msgs = [i.to_bytes(8, "little") for i in range(6)]
+    pks = [o.public_from_seed(s) for s in seeds]
+    sigs = [o.sign(s, m) for s, m in zip(seeds, msgs)]
+    zseed = bytes(range(32))
+    assert nw_ref.verify_batch_msgs(msgs, pks, sigs, zseed, 3)
+    assert o.verify_batch_z(msgs, sigs, pks, o.batch_coefficients(zseed, 3, 6))
+    bad = list(sigs)
+    bad[2] = o.sign(seeds[2], b"x")
+    assert not nw_ref.verify_batch_msgs(msgs, pks, bad, zseed, 3)
+    assert not o.verify_batch_z(msgs, bad, pks, o.batch_coefficients(zseed, 3, 6))

@@ -27,7 +27,7 @@ template <int W>
 static uint32_t build_comb_w(const uint32_t raw[8], uint32_t* bases, uint32_t* tab) {
     const uint32_t info = key_prep_one<W>(raw, bases);
     for (uint32_t pos = 0; pos < (uint32_t)comb_pos(W); ++pos)
-        for (uint32_t e = 0; e < (uint32_t)comb_ent(W); ++e) comb_entry_one<W>(bases, pos, e, tab);
+        for (uint32_t c = 0; c < (uint32_t)(comb_ent(W) + 7) / 8; ++c) comb_chunk_build<W, 8>(bases, pos, c, tab);
     return info;
 }
 
@@ -35,7 +35,7 @@ template <int W>
 static ge_p3 compute_P_w(int w, const uint32_t S[8], const uint32_t h[8], bool sok, const uint32_t* btab,
                          const uint32_t* atab) {
     (void)w;
-    return compute_P<W>(S, h, sok, btab, atab);
+    return compute_P<W, 16>(S, h, sok, btab, atab);   // host harness: basepoint comb at w16
 }
 
 extern "C" {
@@ -191,7 +191,7 @@ void hc_sign32(const uint8_t* seed, const uint8_t* msg32, const uint32_t* btab, 
     uint32_t s[8], m[8], p[8], g[16];
     b2w(s, seed);
     b2w(m, msg32);
-    sign_one<8>(s, m, btab, p, g);
+    sign_one<8, 16>(s, m, btab, p, g);
     std::memcpy(pk, p, 32);
     std::memcpy(sig, g, 64);
 }
