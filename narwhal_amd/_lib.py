@@ -12,7 +12,8 @@ import threading
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnwcrypto.so")
+# NWCRYPTO_LIB: alternative build of the same library (A/B kernel experiments, tools/ only)
+LIB_PATH = os.environ.get("NWCRYPTO_LIB") or os.path.join(_HERE, "libnwcrypto.so")
 
 NW_OK, NW_ERR_SIG, NW_ERR_ARG, NW_ERR_DEVICE, NW_ERR_NOMEM = 0, 1, 2, 3, 4
 F_S_OK, F_A_OK, F_MATCH, F_STRICT, F_A_SMALL, F_R_SMALL = 0x1, 0x2, 0x4, 0x8, 0x10, 0x20

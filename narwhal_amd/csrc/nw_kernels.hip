@@ -55,8 +55,13 @@ __device__ __forceinline__ void coeff_z(const VerifyParams& a, uint32_t i, uint3
 // ------------------------------------------------------------------------------------ verify (P_i)
 // One lane per signature: P_i = s_i B - h_i A_i, written as (X, Y, Z) to pbuf; partial flags
 // (S ok, A ok, A small, torsion coefficient for torsion keys).
+#ifdef NW_VERIFY_WAVES
+#define NW_VERIFY_BOUNDS __launch_bounds__(256, NW_VERIFY_WAVES)
+#else
+#define NW_VERIFY_BOUNDS __launch_bounds__(256)
+#endif
 template <int MSGMODE, int WA>
-__global__ void __launch_bounds__(256) k_verify(VerifyParams a) {
+__global__ void NW_VERIFY_BOUNDS k_verify(VerifyParams a) {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.n) return;
     // signer-grouped order: the 64 lanes of a wave mostly share one key table (TLB / cache locality)
@@ -172,31 +177,41 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
     if (L >= NL) return;
     const uint32_t cnt = (a.n - L + NL - 1) / NL;   // columns L + k NL < n
     const size_t n = a.n;
+    // Both chains are fully unrolled over FINISH_K (guarded by cnt) so the column loads are
+    // independent of the running products and issue ahead of them: with one wave per SIMD the
+    // kernel is latency-bound, and a load inside the serial chain would stall it every step.
     fe acc = fe_one();
-    for (uint32_t k = 0; k < cnt; ++k) {
-        const size_t g = L + (size_t)k * NL;
-        acc = fe_mul(acc, load_fe_soa(a.pbuf + 20 * n, n, g));
-        store_fe_soa(a.pre, n, g, acc);
+#pragma unroll
+    for (int k = 0; k < FINISH_K; ++k) {
+        if ((uint32_t)k < cnt) {
+            const size_t g = L + (size_t)k * NL;
+            acc = fe_mul(acc, load_fe_soa(a.pbuf + 20 * n, n, g));
+            store_fe_soa(a.pre, n, g, acc);
+        }
     }
     fe inv = fe_invert(acc);
-    for (int k = (int)cnt - 1; k >= 0; --k) {
-        const size_t g = L + (size_t)k * NL;
-        fe zi = inv;
-        if (k > 0) {
-            zi = fe_mul(inv, load_fe_soa(a.pre, n, g - NL));
-            inv = fe_mul(inv, load_fe_soa(a.pbuf + 20 * n, n, g));
+#pragma unroll
+    for (int k = FINISH_K - 1; k >= 0; --k) {
+        if ((uint32_t)k < cnt) {
+            const size_t g = L + (size_t)k * NL;
+            fe zi = inv;
+            if (k > 0) {
+                zi = fe_mul(inv, load_fe_soa(a.pre, n, g - NL));
+                inv = fe_mul(inv, load_fe_soa(a.pbuf + 20 * n, n, g));
+            }
+            const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
+            uint32_t R[8];
+            load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
+            uint32_t f = finish_flags(load_fe_soa(a.pbuf, n, g), load_fe_soa(a.pbuf + 10 * n, n, g), zi, R,
+                                      a.flags[i]);
+            if (a.batch_mode && (f & (NW_F_S_OK | NW_F_A_OK)) == (NW_F_S_OK | NW_F_A_OK) && !(f & NW_F_MATCH)) {
+                f |= NW_F_SLOW;
+                const uint32_t t = atomicAdd(a.slow_count, 1u);
+                a.slow_list[t] = i;
+                a.slow_slot[i] = t;
+            }
+            a.flags[i] = f;
         }
-        const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
-        uint32_t R[8];
-        load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
-        uint32_t f = finish_flags(load_fe_soa(a.pbuf, n, g), load_fe_soa(a.pbuf + 10 * n, n, g), zi, R, a.flags[i]);
-        if (a.batch_mode && (f & (NW_F_S_OK | NW_F_A_OK)) == (NW_F_S_OK | NW_F_A_OK) && !(f & NW_F_MATCH)) {
-            f |= NW_F_SLOW;
-            const uint32_t t = atomicAdd(a.slow_count, 1u);
-            a.slow_list[t] = i;
-            a.slow_slot[i] = t;
-        }
-        a.flags[i] = f;
     }
 }
 
@@ -222,21 +237,32 @@ __global__ void __launch_bounds__(256) k_slow_sig(VerifyParams a) {
 }
 
 // Per-certificate verdict: definitive Err on any bad S / undecodable A / undecodable R, else the
-// exact remaining batch sum (usually empty) must be the identity.
+// exact remaining batch sum (usually empty) must be the identity.  One 64-lane wave per
+// certificate: lanes stride over the votes (coalesced flag reads), wave reductions combine them;
+// the exact sum over slow-path terms (failing certificates only) runs on lane 0.
 __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= a.ncerts) return;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (c >= a.ncerts) return;   // whole wave exits together
     const uint32_t first = a.cert_first[c], nv = a.cert_n[c];
     bool bad = false, slow = false;
     uint32_t tsum = 0;
     uint64_t stake = 0;
-    for (uint32_t v = 0; v < nv; ++v) {
+    for (uint32_t v = lane; v < nv; v += 64) {
         const uint32_t f = a.flags[first + v];
         bad = bad || ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) || (f & NW_F_R_BAD);
         slow = slow || (f & NW_F_SLOW);
         tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
         if (f & NW_F_STRICT) stake += a.stake[a.signer[first + v]];
     }
+    bad = __any(bad);
+    slow = __any(slow);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        tsum += __shfl_xor(tsum, off, 64);
+        stake += __shfl_xor(stake, off, 64);
+    }
+    if (lane != 0) return;
     bool ok;
     if (bad) {
         ok = false;
@@ -451,7 +477,7 @@ hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint3
 
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
     if (p.ncerts == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_cert_finalize, dim3(blocks_for(p.ncerts, 256)), dim3(256), 0, st, p);
+    hipLaunchKernelGGL(k_cert_finalize, dim3(blocks_for((uint64_t)p.ncerts * 64, 256)), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 
