@@ -53,27 +53,29 @@ def unpack_bits(packed, n: int):
 def allgather_verdicts(ok_local, stake_local, ranges: List[Tuple[int, int]], group=None):
     """All-gather per-shard verdicts (bit-packed) and accepted stake into global [ncerts] tensors.
 
-    ``ok_local``: uint8 [c1 - c0]; ``stake_local``: int64 [c1 - c0] (this rank's range).  Works on
-    any torch.distributed backend (RCCL on GPU tensors, gloo on CPU tensors for tests)."""
+    ``ok_local``: uint8 [c1 - c0]; ``stake_local``: int64 [c1 - c0] (this rank's range).  One
+    collective per call: each rank contributes [bitmap | stake as bytes] in a single uint8 buffer,
+    so the exchange is one latency-bound all_gather (RCCL over xGMI on GPU tensors, gloo on CPU
+    tensors for the tests)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     maxc = max(c1 - c0 for c0, c1 in ranges)
-    maxb = (maxc + 7) // 8
+    maxb = (maxc + 63) // 64 * 8           # bitmap bytes, padded so the stake words stay 8-B aligned
     dev = ok_local.device
-    bits = torch.zeros(maxb, dtype=torch.uint8, device=dev)
+    buf = torch.zeros(maxb + 8 * maxc, dtype=torch.uint8, device=dev)
     pb = pack_bits(ok_local)
-    bits[:pb.shape[0]] = pb
-    stake = torch.zeros(maxc, dtype=torch.int64, device=dev)
-    stake[:stake_local.shape[0]] = stake_local
-    gb = [torch.empty_like(bits) for _ in range(world)]
-    gs = [torch.empty_like(stake) for _ in range(world)]
-    dist.all_gather(gb, bits, group=group)
-    dist.all_gather(gs, stake, group=group)
+    buf[:pb.shape[0]] = pb
+    n = stake_local.shape[0]
+    if n:
+        buf[maxb:maxb + 8 * n] = stake_local.to(torch.int64).contiguous().view(torch.uint8)
+    gathered = [torch.empty_like(buf) for _ in range(world)]
+    dist.all_gather(gathered, buf, group=group)
     oks, stakes = [], []
     for r, (c0, c1) in enumerate(ranges):
-        oks.append(unpack_bits(gb[r], c1 - c0))
-        stakes.append(gs[r][:c1 - c0])
+        g = gathered[r]
+        oks.append(unpack_bits(g[:maxb], c1 - c0))
+        stakes.append(g[maxb:maxb + 8 * (c1 - c0)].view(torch.int64))
     return torch.cat(oks), torch.cat(stakes)
 
 

@@ -46,6 +46,9 @@ def main():
         if "GRBM_GUI_ACTIVE" in row:
             row["max_dispatch_us"] = max(dur[k])
             row["effective_clock_ghz"] = row["GRBM_GUI_ACTIVE"] / 8 / (max(dur[k]) * 1e3)
+            if "SQ_THREAD_CYCLES_VALU" in row:
+                # VALU busy cycles per SIMD (thread-cycles / 64 lanes) over the kernel's cycles x 1024 SIMDs
+                row["valu_utilization"] = (row["SQ_THREAD_CYCLES_VALU"] / 64.0) / (row["GRBM_GUI_ACTIVE"] / 8 * 1024)
         out["kernels"][k] = row
     kv = [k for k in out["kernels"] if k.startswith("nw::k_verify")]
     if kv:
