@@ -88,6 +88,16 @@ NW_HD fe fe_sub(const fe& f, const fe& g) {
     return h;
 }
 
+// h = f - g without the carry pass (k_f <= 1, g <= 4p limb-wise): limbs < 1.25 * 2^28 / 2^27,
+// i.e. k = 5.  Only valid as the FIRST operand of fe_mul with a second operand of k <= 6/... such
+// that k_f * k_g <= 32 (see the limb-size discipline above): 5 x 1 and 5 x 2 are used.
+NW_HD fe fe_sub_loose(const fe& f, const fe& g) {
+    fe h;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] + FE_4P[i] - g.v[i];
+    return h;
+}
+
 // h = -f for tight f, k = 2 output (no carry): 2p - f.
 NW_HD fe fe_neg(const fe& f) {
     fe h;

@@ -53,12 +53,14 @@ NW_HD ge_precomp ge_precomp_identity() {
 }
 
 // p + q (mixed).  Limb budget: (Y1+X1) k=2, D = 2Z1 k=2, G = D + C k=3, xy2d may be k=2 (negated).
+// (Y1-X1) and e = b - a skip the carry pass (fe_sub_loose, k = 5): each only ever feeds fe_mul as
+// the first operand against a second operand of k <= 2 (ymx tight; f tight; h k=2): 5 x 2 <= 32.
 NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) {
-    const fe a = fe_mul(fe_sub(p.Y, p.X), q.ymx);
+    const fe a = fe_mul(fe_sub_loose(p.Y, p.X), q.ymx);
     const fe b = fe_mul(fe_add(p.Y, p.X), q.ypx);
     const fe c = fe_mul(p.T, q.xy2d);
     const fe d = fe_add(p.Z, p.Z);
-    const fe e = fe_sub(b, a);
+    const fe e = fe_sub_loose(b, a);
     const fe h = fe_add(b, a);
     const fe f = fe_sub(d, c);
     const fe g = fe_add(d, c);
