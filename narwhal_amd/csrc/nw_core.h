@@ -395,7 +395,7 @@ NW_HD void comb_chunk_build(const uint32_t* bases, uint32_t pos, uint32_t c, uin
             if ((uint32_t)k + 1 < cnt) Q = ge_add(Q, bc);
         }
     }
-    fe inv = fe_invert(acc);
+    fe inv = fe_invert_sg(acc);
 #pragma unroll
     for (int k = CH - 1; k >= 0; --k) {
         if ((uint32_t)k < cnt) {

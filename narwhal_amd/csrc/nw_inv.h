@@ -1,0 +1,184 @@
+// Field inversion in GF(2^255 - 19) by Bernstein-Yang "safegcd" divsteps (constant iteration count,
+// branch-free, so every lane of a wave runs the same instruction stream).
+//
+// Why: the Fermat chain (fe_invert: 254 squarings + 11 multiplications) is one long dependent
+// sequence of ~95k VALU cycles per lane; k_finish pays one inversion per chain of FINISH_K
+// signatures, and a single-certificate submission pays it on its critical path.  safegcd replaces
+// it with 20 batches of 30 divsteps on the low 32 bits (plain 32-bit ops) plus, per batch, one
+// 2x2 transition-matrix application to (f, g) and to the Bezout pair (d, e) (signed 32x32->64
+// multiply-accumulates over nine 30-bit limbs).
+//
+// Algorithm (Bernstein & Yang, "Fast constant-time gcd computation and modular inversion", 2019,
+// with the delta = 1/2 start and the 590-divstep bound for 256-bit moduli): f = p, g = x, d = 0,
+// e = 1; each divstep maps (delta, f, g) to (1 - delta, g, (g - f)/2) when delta > 0 and g is
+// odd, else to (1 + delta, f, (g + (g mod 2) f)/2), with (d, e) tracking f = d x, g = e x (mod p)
+// scaled by 2^-steps.  After 600 divsteps g = 0 and f = +-1, so x^-1 = +-d.  Here zeta = -(delta
+// + 1/2) so the "delta > 0" test is a sign test.
+//
+// Signed-30 limbs: value = sum v[i] 2^(30 i), nine limbs (270 bits), limbs in (-2^30, 2^30)
+// except the top one, which carries the sign.
+#pragma once
+#include <cstdint>
+#include "nw_field.h"
+
+namespace nw {
+
+struct s30 {
+    int32_t v[9];
+};
+
+static constexpr int32_t S30_M = 0x3FFFFFFF;
+// p = 2^255 - 19 in signed-30 limbs, and p^-1 mod 2^30.
+static constexpr int32_t S30_P[9] = {0x3FFFFFED, 0x3FFFFFFF, 0x3FFFFFFF, 0x3FFFFFFF, 0x3FFFFFFF,
+                                     0x3FFFFFFF, 0x3FFFFFFF, 0x3FFFFFFF, 0x7FFF};
+static constexpr uint32_t S30_PINV = 0x179435E5u;
+
+struct s30_trans {
+    int32_t u, v, q, r;
+};
+
+// 30 divsteps on the low 32 bits of f (odd) and g.  Returns the new zeta; t maps (f, g) to
+// 2^30 (f', g').  Matrix entries stay in [-2^30, 2^30]; kept unsigned so the shifts are defined.
+NW_HD int32_t s30_divsteps(int32_t zeta, uint32_t f, uint32_t g, s30_trans& t) {
+    uint32_t u = 1, v = 0, q = 0, r = 1;
+#pragma unroll
+    for (int i = 0; i < 30; ++i) {
+        const uint32_t c1 = (uint32_t)(zeta >> 31);   // all-ones iff zeta < 0 (delta > 0)
+        const uint32_t c2 = 0u - (g & 1u);            // all-ones iff g odd
+        const uint32_t x = (f ^ c1) - c1;             // -f, -u, -v when delta > 0
+        const uint32_t y = (u ^ c1) - c1;
+        const uint32_t z = (v ^ c1) - c1;
+        g += x & c2;
+        q += y & c2;
+        r += z & c2;
+        const uint32_t c3 = c1 & c2;                  // swap case
+        zeta = (int32_t)(((uint32_t)zeta ^ c3) - 1u);
+        f += g & c3;
+        u += q & c3;
+        v += r & c3;
+        g >>= 1;
+        u += u;
+        v += v;
+    }
+    t.u = (int32_t)u;
+    t.v = (int32_t)v;
+    t.q = (int32_t)q;
+    t.r = (int32_t)r;
+    return zeta;
+}
+
+// (f, g) <- t (f, g) / 2^30 (exact: the low 30 bits of both products are zero by construction).
+NW_HD void s30_update_fg(s30& f, s30& g, const s30_trans& t) {
+    int64_t cf = (int64_t)t.u * f.v[0] + (int64_t)t.v * g.v[0];
+    int64_t cg = (int64_t)t.q * f.v[0] + (int64_t)t.r * g.v[0];
+    cf >>= 30;
+    cg >>= 30;
+#pragma unroll
+    for (int i = 1; i < 9; ++i) {
+        const int32_t fi = f.v[i], gi = g.v[i];
+        cf += (int64_t)t.u * fi + (int64_t)t.v * gi;
+        cg += (int64_t)t.q * fi + (int64_t)t.r * gi;
+        f.v[i - 1] = (int32_t)cf & S30_M;
+        g.v[i - 1] = (int32_t)cg & S30_M;
+        cf >>= 30;
+        cg >>= 30;
+    }
+    f.v[8] = (int32_t)cf;
+    g.v[8] = (int32_t)cg;
+}
+
+// (d, e) <- (t (d, e) + p (md, me)) / 2^30 with md, me chosen so the division is exact; keeps
+// d, e in (-2p, p) given they start there.
+NW_HD void s30_update_de(s30& d, s30& e, const s30_trans& t) {
+    const int32_t sd = d.v[8] >> 31, se = e.v[8] >> 31;
+    int32_t md = (t.u & sd) + (t.v & se);
+    int32_t me = (t.q & sd) + (t.r & se);
+    int64_t cd = (int64_t)t.u * d.v[0] + (int64_t)t.v * e.v[0];
+    int64_t ce = (int64_t)t.q * d.v[0] + (int64_t)t.r * e.v[0];
+    md -= (int32_t)((S30_PINV * (uint32_t)cd + (uint32_t)md) & (uint32_t)S30_M);
+    me -= (int32_t)((S30_PINV * (uint32_t)ce + (uint32_t)me) & (uint32_t)S30_M);
+    cd += (int64_t)S30_P[0] * md;
+    ce += (int64_t)S30_P[0] * me;
+    cd >>= 30;
+    ce >>= 30;
+#pragma unroll
+    for (int i = 1; i < 9; ++i) {
+        const int32_t di = d.v[i], ei = e.v[i];
+        cd += (int64_t)t.u * di + (int64_t)t.v * ei + (int64_t)S30_P[i] * md;
+        ce += (int64_t)t.q * di + (int64_t)t.r * ei + (int64_t)S30_P[i] * me;
+        d.v[i - 1] = (int32_t)cd & S30_M;
+        e.v[i - 1] = (int32_t)ce & S30_M;
+        cd >>= 30;
+        ce >>= 30;
+    }
+    d.v[8] = (int32_t)cd;
+    e.v[8] = (int32_t)ce;
+}
+
+// r in (-2p, p) -> r * sign(sgn) mod p in [0, p), limbs in [0, 2^30).
+NW_HD void s30_normalize(s30& r, int32_t sgn) {
+    int32_t m = r.v[8] >> 31;   // add p if negative
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] += S30_P[i] & m;
+    const int32_t n = sgn >> 31;   // negate if f ended at -1
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] = (r.v[i] ^ n) - n;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        r.v[i + 1] += r.v[i] >> 30;
+        r.v[i] &= S30_M;
+    }
+    m = r.v[8] >> 31;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) r.v[i] += S30_P[i] & m;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        r.v[i + 1] += r.v[i] >> 30;
+        r.v[i] &= S30_M;
+    }
+}
+
+// z^-1 mod p (0 -> 0), same result as fe_invert.
+NW_HD fe fe_invert_sg(const fe& z) {
+    uint32_t w[8];
+    fe_tobytes_w(w, z);
+    s30 g;
+    g.v[0] = (int32_t)(w[0] & S30_M);
+    g.v[1] = (int32_t)(((w[0] >> 30) | (w[1] << 2)) & S30_M);
+    g.v[2] = (int32_t)(((w[1] >> 28) | (w[2] << 4)) & S30_M);
+    g.v[3] = (int32_t)(((w[2] >> 26) | (w[3] << 6)) & S30_M);
+    g.v[4] = (int32_t)(((w[3] >> 24) | (w[4] << 8)) & S30_M);
+    g.v[5] = (int32_t)(((w[4] >> 22) | (w[5] << 10)) & S30_M);
+    g.v[6] = (int32_t)(((w[5] >> 20) | (w[6] << 12)) & S30_M);
+    g.v[7] = (int32_t)(((w[6] >> 18) | (w[7] << 14)) & S30_M);
+    g.v[8] = (int32_t)(w[7] >> 16);
+    s30 f, d, e;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        f.v[i] = S30_P[i];
+        d.v[i] = 0;
+        e.v[i] = 0;
+    }
+    e.v[0] = 1;
+    int32_t zeta = -1;
+#pragma nounroll
+    for (int it = 0; it < 20; ++it) {
+        s30_trans t;
+        zeta = s30_divsteps(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+        s30_update_de(d, e, t);
+        s30_update_fg(f, g, t);
+    }
+    s30_normalize(d, f.v[8]);
+    // [0, p) in 30-bit limbs -> 8 LE words -> radix 2^25.5
+    w[0] = (uint32_t)d.v[0] | ((uint32_t)d.v[1] << 30);
+    w[1] = ((uint32_t)d.v[1] >> 2) | ((uint32_t)d.v[2] << 28);
+    w[2] = ((uint32_t)d.v[2] >> 4) | ((uint32_t)d.v[3] << 26);
+    w[3] = ((uint32_t)d.v[3] >> 6) | ((uint32_t)d.v[4] << 24);
+    w[4] = ((uint32_t)d.v[4] >> 8) | ((uint32_t)d.v[5] << 22);
+    w[5] = ((uint32_t)d.v[5] >> 10) | ((uint32_t)d.v[6] << 20);
+    w[6] = ((uint32_t)d.v[6] >> 12) | ((uint32_t)d.v[7] << 18);
+    w[7] = ((uint32_t)d.v[7] >> 14) | ((uint32_t)d.v[8] << 16);
+    return fe_frombytes_w(w);
+}
+
+}  // namespace nw

@@ -13,7 +13,10 @@ static constexpr uint32_t KI_TORSION_SHIFT = 4;   // 3 bits: t with A^t = t * T8
 static constexpr uint32_t NW_F_TCOEF_SHIFT = 8;   // 3 bits of per-signature torsion coefficient
 static constexpr int SLOW_WORDS = 40;             // slow-path record: extended point z_i (R_i - P_i)
 static constexpr int PBUF_WORDS = 32;             // per-signature P record: X, Y, Z (30 words) + pad
-static constexpr int FINISH_K = 16;               // signatures per lane in the batch-inversion kernel
+#ifndef NW_FINISH_K
+#define NW_FINISH_K 16
+#endif
+static constexpr int FINISH_K = NW_FINISH_K;      // signatures per lane in the batch-inversion kernel
 
 struct VerifyParams {
     uint32_t n;                    // signatures

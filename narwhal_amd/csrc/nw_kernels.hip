@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
             store_fe_soa(a.pre, n, g, acc);
         }
     }
-    fe inv = fe_invert(acc);
+    fe inv = fe_invert_sg(acc);
 #pragma unroll
     for (int k = FINISH_K - 1; k >= 0; --k) {
         if ((uint32_t)k < cnt) {

@@ -8,6 +8,7 @@
 // exact group elements curve25519-dalek computes for any decodable input, torsion included.
 #pragma once
 #include "nw_field.h"
+#include "nw_inv.h"
 #include "nw_scalar.h"
 
 namespace nw {
@@ -188,7 +189,7 @@ NW_HD bool ge_decompress(ge_p3& out, const uint32_t w[8]) {
 
 // Canonical compressed encoding (8 LE words): y with the sign of x in bit 255.
 NW_HD void ge_compress_w(uint32_t out[8], const ge_p3& p) {
-    const fe zi = fe_invert(p.Z);
+    const fe zi = fe_invert_sg(p.Z);
     uint32_t xw[8];
     fe_tobytes_w(xw, fe_mul(p.X, zi));
     fe_tobytes_w(out, fe_mul(p.Y, zi));
@@ -231,7 +232,7 @@ NW_HD ge_precomp ge_precomp_from_words(const uint32_t* w) {
 
 // Affine Niels form of p (one inversion); tight limbs.
 NW_HD ge_precomp ge_to_precomp(const ge_p3& p) {
-    const fe zi = fe_invert(p.Z);
+    const fe zi = fe_invert_sg(p.Z);
     const fe x = fe_mul(p.X, zi);
     const fe y = fe_mul(p.Y, zi);
     ge_precomp q;

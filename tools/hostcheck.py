@@ -41,6 +41,9 @@ def check_field(rng, n):
     for _ in range(max(1, n // 20)):
         a = rng.randrange(1, P)
         assert call_fe(lib.hc_fe_invert, a) == pow(a, P - 2, P), "invert"
+        assert call_fe(lib.hc_fe_invert_sg, a) == pow(a, P - 2, P), "invert (safegcd)"
+    for a in [0, 1, 2, P - 1, P, P + 1, (1 << 255) - 1, 19, (1 << 254), (1 << 255) - 20]:
+        assert call_fe(lib.hc_fe_invert_sg, a) == pow(a, P - 2, P), ("invert (safegcd)", a)
         assert call_fe(lib.hc_fe_pow22523, a) == pow(a, (P - 5) // 8, P), "pow22523"
     # all-ones limbs stress
     mx = (1 << 255) - 1
