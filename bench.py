@@ -236,7 +236,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     eng.profile_enable(False)
-    kms, kn = eng.profile_read()
+    kms, kn, ksigs = eng.profile_read()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -251,19 +251,23 @@ def main():
 
     if rank == 0:
         avg_launch_s = (kms / kn) / 1e3 if kn else float("nan")
+        if ksigs is None:                              # library without nw_profile_read_sigs (A/B runs)
+            ksigs = cs.nsigs * kn
+        sigs_per_launch = ksigs / kn if kn else 0.0
         kw = eng.key_window()
         fm = kverify_fm_per_sig(kw)
         peak = valu_peak_mad_per_s() / 1e12
-        achieved = cs.nsigs * fm * MADS_PER_FM / avg_launch_s / 1e12
+        achieved = sigs_per_launch * fm * MADS_PER_FM / avg_launch_s / 1e12
         v1 = COST_MODEL_V1_FM.get(args.votes)
         roofline = {
             "bound": "valu", "kernel": "k_verify", "achieved": achieved, "peak": peak, "unit": "TMAD/s",
             "frac": achieved / peak, "traffic": traffic_per_launch(),
             "avg_launch_ms": avg_launch_s * 1e3, "launches": kn,
-            "work_model": "%d sigs/launch x %d FM/sig (7 FM per mixed addition x (%d basepoint + %d key) comb "
-                          "positions, key window %d) x 100 u32 MADs; SHA-512/mod-l/recoding VALU work not counted; "
-                          "peak = measured v_mad_u64_u32 rate" % (cs.nsigs, fm, comb_pos(B_WINDOW), comb_pos(kw), kw),
-            "dalek_equiv": {"fm_per_sig": v1, "TMADps": (cs.nsigs * v1 * MADS_PER_FM / avg_launch_s / 1e12)
+            "work_model": "%.0f sigs/launch (%d launches per step) x %d FM/sig (7 FM per mixed addition x (%d basepoint "
+                          "+ %d key) comb positions, key window %d) x 100 u32 MADs; SHA-512/mod-l/recoding VALU work "
+                          "not counted; peak = measured v_mad_u64_u32 rate"
+                          % (sigs_per_launch, kn // args.steps, fm, comb_pos(B_WINDOW), comb_pos(kw), kw),
+            "dalek_equiv": {"fm_per_sig": v1, "TMADps": (sigs_per_launch * v1 * MADS_PER_FM / avg_launch_s / 1e12)
                             if v1 else None,
                             "note": "SURVEY §8(d) cost model v1 = dalek's MSM work per signature; the comb "
                                     "algorithm needs %.1fx fewer FM" % (v1 / fm) if v1 else ""},

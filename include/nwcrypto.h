@@ -153,6 +153,9 @@ int nw_sign_many_dev(nw_ctx* ctx, const uint8_t* d_seed32, const uint8_t* d_msgs
  * back (synchronizing those events) the summed device time and launch count, then reset. */
 int nw_profile_enable(nw_ctx* ctx, int on);
 int nw_profile_read(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launches);
+/* Same, plus the signatures covered by those launches (the roofline's work per launch). */
+int nw_profile_read_sigs(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launches,
+                         uint64_t* verify_sigs);
 
 /* Library build identifier (gfx target, build date). */
 const char* nw_version(void);

@@ -33,6 +33,9 @@ class NwCert(ctypes.Structure):
     _fields_ = [("first_vote", ctypes.c_uint32), ("n_votes", ctypes.c_uint32)]
 
 
+_OPTIONAL = {"nw_profile_read_sigs"}
+
+
 def _load() -> ctypes.CDLL:
     if not os.path.exists(LIB_PATH):
         raise ImportError(
@@ -59,9 +62,12 @@ def _load() -> ctypes.CDLL:
         "nw_sign_many_dev": (I, [P, P, P, S, S, P, P, P]),
         "nw_profile_enable": (I, [P, I]),
         "nw_profile_read": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]),
+        "nw_profile_read_sigs": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "nw_version": (ctypes.c_char_p, []),
     }
     for name, (res, args) in sig.items():
+        if name in _OPTIONAL and not hasattr(lib, name):
+            continue   # older library build loaded for an A/B run (NWCRYPTO_LIB)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -296,11 +302,17 @@ class Engine:
         self.check(LIB.nw_profile_enable(self._ctx, 1 if on else 0), "nw_profile_enable")
 
     def profile_read(self):
-        """(summed k_verify device ms, launches) since the last read; synchronizes the events."""
+        """(summed k_verify device ms, launches, signatures in those launches) since the last read;
+        synchronizes the events."""
         ms = ctypes.c_double(0)
         n = ctypes.c_uint64(0)
-        self.check(LIB.nw_profile_read(self._ctx, ctypes.byref(ms), ctypes.byref(n)), "nw_profile_read")
-        return ms.value, n.value
+        sigs = ctypes.c_uint64(0)
+        if not hasattr(LIB, "nw_profile_read_sigs"):
+            self.check(LIB.nw_profile_read(self._ctx, ctypes.byref(ms), ctypes.byref(n)), "nw_profile_read")
+            return ms.value, n.value, None
+        self.check(LIB.nw_profile_read_sigs(self._ctx, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(sigs)),
+                   "nw_profile_read_sigs")
+        return ms.value, n.value, sigs.value
 
     def sha512_many_dev(self, d_base, d_off, d_len, n, d_out, stream):
         self.check(LIB.nw_sha512_many_dev(self._ctx, d_base, d_off, d_len, n, d_out, stream), "nw_sha512_many_dev")

@@ -2,6 +2,7 @@
 // and the launch sequences.  No CPU compute path: every verdict and digest comes from the GPU.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -47,6 +48,7 @@ struct DevBuf {
 struct nw_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    uint32_t finish_k = FINISH_K;   // k_finish signatures per lane
     std::mutex mu;
     std::string last_error;
     // basepoint comb
@@ -67,6 +69,7 @@ struct nw_ctx {
     bool prof_on = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
     size_t prof_used = 0;
+    uint64_t prof_sigs = 0;
     // workspace
     DevBuf w_bases, w_sig, w_signer, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len,
         w_flags, w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_stake_out, w_ok, w_misc,
@@ -92,6 +95,16 @@ int fail(nw_ctx* c, hipError_t e, const char* what) {
 const uint8_t kBaseEnc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                               0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                               0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
+
+// k_finish signatures per lane (NW_FK overrides it for tuning; 1..FINISH_K).  Measured on MI355X:
+// splitting a batch into chunks so k_finish of one chunk overlaps k_verify of the next on a second
+// stream was slower (623 vs 712 M sigs/s at C2: the co-running k_finish waves take VGPR slots from
+// the VALU-bound k_verify and every chunk pays a tail), so a batch is one k_verify + one k_finish.
+uint32_t finish_k() {
+    const char* e = std::getenv("NW_FK");
+    const long k = e ? std::strtol(e, nullptr, 10) : 0;
+    return k >= 1 && k <= FINISH_K ? (uint32_t)k : (uint32_t)FINISH_K;
+}
 
 constexpr size_t KEY_CACHE_BUDGET = 160ull << 30;  // bytes of HBM for key tables by default (of 288 GB)
 constexpr size_t kGroupMinSigs = 16384;            // group signatures by signer above this batch size
@@ -282,6 +295,9 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
                "signer grouping");
         vp.perm = ctx->w_perm.as<uint32_t>();
     }
+    vp.g0 = 0;
+    vp.gn = (uint32_t)nsigs;
+    vp.fk = ctx->finish_k;
     hipEvent_t ev_stop = nullptr;
     if (ctx->prof_on && nsigs) {
         if (ctx->prof_used == ctx->prof_events.size()) {
@@ -293,6 +309,7 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
         NW_TRY(hipEventRecord(ctx->prof_events[ctx->prof_used].first, st), "hipEventRecord");
         ev_stop = ctx->prof_events[ctx->prof_used].second;
         ++ctx->prof_used;
+        ctx->prof_sigs += nsigs;
     }
     NW_TRY(launch_verify(vp, msgmode, ctx->key_window, st), "k_verify");
     if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");   // brackets k_verify alone
@@ -401,6 +418,7 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
         return NW_ERR_ARG;
     }
     ctx->device = dev;
+    ctx->finish_k = finish_k();
     if (opts && opts->max_keys) {
         ctx->max_keys = opts->max_keys;
         ctx->max_keys_user = true;
@@ -454,6 +472,7 @@ void nw_ctx_destroy(nw_ctx* ctx) {
         (void)hipEventDestroy(ev.first);
         (void)hipEventDestroy(ev.second);
     }
+
     for (uint32_t* p : {ctx->d_btab, ctx->d_keys_raw, ctx->d_key_info, ctx->d_stake, ctx->d_key_tab})
         if (p) (void)hipFree(p);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -468,6 +487,10 @@ int nw_profile_enable(nw_ctx* ctx, int on) {
 }
 
 int nw_profile_read(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launches) {
+    return nw_profile_read_sigs(ctx, verify_ms_total, verify_launches, nullptr);
+}
+
+int nw_profile_read_sigs(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launches, uint64_t* verify_sigs) {
     if (!ctx) return NW_ERR_ARG;
     std::lock_guard<std::mutex> g(ctx->mu);
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
@@ -480,7 +503,9 @@ int nw_profile_read(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launc
     }
     if (verify_ms_total) *verify_ms_total = total;
     if (verify_launches) *verify_launches = ctx->prof_used;
+    if (verify_sigs) *verify_sigs = ctx->prof_sigs;
     ctx->prof_used = 0;
+    ctx->prof_sigs = 0;
     return NW_OK;
 }
 

@@ -233,46 +233,55 @@ NW_HD void store_fe_soa(uint32_t* p, size_t n, size_t g, const fe& f) {
     for (int k = 0; k < 10; ++k) p[k * n + g] = f.v[k];
 }
 
-// P's X, Y, Z as 30 SoA rows (X rows 0..9, Y 10..19, Z 20..29).
-NW_HD void store_xyz_soa(uint32_t* p, size_t n, size_t g, const ge_p3& P) {
+// k_verify -> k_finish record, struct-of-arrays in processing order: X rows 0..9, Z rows 10..19,
+// partial flags row 20 (PREC_ROWS rows of n words).
+static constexpr int PREC_ROWS = 21;
+static constexpr int PREC_FLAGS_ROW = 20;
+static_assert(PREC_ROWS <= PBUF_WORDS, "pbuf workspace rows");
+static constexpr uint32_t PF_YMATCH = 1u << 20;   // internal: y_R Z == Y (projective)
+static constexpr uint32_t PF_RSIGN = 1u << 21;    // internal: R's sign bit (bit 255)
+static constexpr uint32_t PF_INTERNAL = PF_YMATCH | PF_RSIGN;
+
+NW_HD void store_prec_soa(uint32_t* p, size_t n, size_t g, const ge_p3& P, uint32_t pflags) {
     store_fe_soa(p, n, g, P.X);
-    store_fe_soa(p + 10 * n, n, g, P.Y);
-    store_fe_soa(p + 20 * n, n, g, P.Z);
+    store_fe_soa(p + 10 * n, n, g, P.Z);
+    p[PREC_FLAGS_ROW * n + g] = pflags;
 }
 
-NW_HD void store_xyz(uint32_t* dst, const ge_p3& P) {
-    store_fe(dst, P.X);
-    store_fe(dst + 10, P.Y);
-    store_fe(dst + 20, P.Z);
-    dst[30] = 0;
-    dst[31] = 0;
-}
-
-// Completes the per-signature flags from P's projective X, Y and zi = 1/Z:
-//   MATCH  <=> R decodes (dalek decompress) and decode(R) == P  (the strict equation R = sB - hA)
-//   STRICT <=> verify_strict accepts (adds: S ok, A ok, neither R nor A of small order)
-NW_HD uint32_t finish_flags(const fe& X, const fe& Y, const fe& zi, const uint32_t R[8], uint32_t partial) {
-    uint32_t xw[8], yw[8];
-    fe_tobytes_w(xw, fe_mul(X, zi));
-    fe_tobytes_w(yw, fe_mul(Y, zi));
-    // R's y (bit 255 cleared) reduced mod p, as FieldElement::from_bytes reads it
+// The half of the encoding match that needs no inversion (run in k_verify, where P is live):
+//   y:  decode(R).y == P.y  <=>  y_R Z == Y  (y_R = R's y field as FieldElement::from_bytes reads
+//       it, i.e. taken mod p); when it holds, R decodes (P.x^2 is the ratio sqrt_ratio_i roots)
+//   R small order (meaningful when MATCH): canonical y_R is one of the five y's of E[8]
+//   R's sign bit, for k_finish's parity check.
+NW_HD uint32_t verify_pflags(const ge_p3& P, const uint32_t R[8], uint32_t partial) {
+    const fe yR = fe_frombytes_w(R);
+    const bool ymatch = fe_iszero(fe_sub(fe_mul(yR, P.Z), P.Y));
     uint32_t yr[8];
-    fe_tobytes_w(yr, fe_frombytes_w(R));
-    const bool x_zero = (xw[0] | xw[1] | xw[2] | xw[3] | xw[4] | xw[5] | xw[6] | xw[7]) == 0;
-    const bool match = words_eq8(yw, yr) && (x_zero || ((xw[0] & 1u) == (R[7] >> 31)));
-    const bool rsmall = y_is_small_order(yw);
-    const bool sok = (partial & NW_F_S_OK) != 0, aok = (partial & NW_F_A_OK) != 0;
-    const bool asmall = (partial & NW_F_A_SMALL) != 0;
-    const bool strict = sok && aok && match && !asmall && !rsmall;
-    return partial | (match ? NW_F_MATCH : 0u) | (strict ? NW_F_STRICT : 0u) | (rsmall ? NW_F_R_SMALL : 0u);
+    fe_tobytes_w(yr, yR);
+    return partial | (ymatch ? PF_YMATCH : 0u) | ((R[7] >> 31) ? PF_RSIGN : 0u) |
+           (y_is_small_order(yr) ? NW_F_R_SMALL : 0u);
 }
 
-// Flags from P (with zi = 1/Z_P) against the signature's R encoding:
+// The other half, after the batch inversion (zi = 1/Z): x = X zi; decode(R) == P iff the y's match
+// and x = 0 or x's parity is R's sign bit (dalek's decompress negates the non-negative root when
+// the sign bit is set, and accepts x = 0 with the sign bit set).
 //   MATCH  <=> R decodes (dalek decompress) and decode(R) == P  (the strict equation R = sB - hA)
 //   STRICT <=> verify_strict accepts (adds: S ok, A ok, neither R nor A of small order)
+NW_HD uint32_t finish_x_flags(const fe& X, const fe& zi, uint32_t pf) {
+    uint32_t xw[8];
+    fe_tobytes_w(xw, fe_mul(X, zi));
+    const bool x_zero = (xw[0] | xw[1] | xw[2] | xw[3] | xw[4] | xw[5] | xw[6] | xw[7]) == 0;
+    const bool match = (pf & PF_YMATCH) && (x_zero || ((xw[0] & 1u) == ((pf & PF_RSIGN) ? 1u : 0u)));
+    const bool sok = (pf & NW_F_S_OK) != 0, aok = (pf & NW_F_A_OK) != 0;
+    const bool asmall = (pf & NW_F_A_SMALL) != 0, rsmall = (pf & NW_F_R_SMALL) != 0;
+    const bool strict = sok && aok && match && !asmall && !rsmall;
+    return (pf & ~PF_INTERNAL) | (match ? NW_F_MATCH : 0u) | (strict ? NW_F_STRICT : 0u);
+}
+
+// Flags from P (with zi = 1/Z_P) against the signature's R encoding (both halves).
 NW_HD uint32_t match_flags(const ge_p3& P, const fe& zi, const uint32_t R[8], bool sok, bool aok, bool asmall) {
-    return finish_flags(P.X, P.Y, zi, R,
-                        (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | (asmall ? NW_F_A_SMALL : 0u));
+    const uint32_t partial = (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | (asmall ? NW_F_A_SMALL : 0u);
+    return finish_x_flags(P.X, zi, verify_pflags(P, R, partial));
 }
 
 // Torsion coefficient of signature i: ((r - z h) mod 8) * t mod 8 with r = z h mod l

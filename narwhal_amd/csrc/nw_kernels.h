@@ -12,14 +12,18 @@ static constexpr uint32_t KI_SMALL = 2u;          // small order
 static constexpr uint32_t KI_TORSION_SHIFT = 4;   // 3 bits: t with A^t = t * T8
 static constexpr uint32_t NW_F_TCOEF_SHIFT = 8;   // 3 bits of per-signature torsion coefficient
 static constexpr int SLOW_WORDS = 40;             // slow-path record: extended point z_i (R_i - P_i)
-static constexpr int PBUF_WORDS = 32;             // per-signature P record: X, Y, Z (30 words) + pad
+static constexpr int PBUF_WORDS = 21;             // per-signature k_verify -> k_finish record (X, Z, flags)
 #ifndef NW_FINISH_K
 #define NW_FINISH_K 16
 #endif
 static constexpr int FINISH_K = NW_FINISH_K;      // signatures per lane in the batch-inversion kernel
 
+static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
+
 struct VerifyParams {
-    uint32_t n;                    // signatures
+    uint32_t n;                    // signatures (also the SoA row stride of pbuf / pre)
+    uint32_t g0, gn;               // processing-order columns [g0, g0 + gn) handled by this launch
+    uint32_t fk;                   // k_finish: signatures per lane (1..FINISH_K)
     uint32_t batch_mode;           // 0: strict flags only; 1: batch bookkeeping (z, slow list)
     const uint8_t* sig;            // [n][64]  R || S
     const uint32_t* signer;        // [n] key-cache slot
@@ -40,7 +44,7 @@ struct VerifyParams {
     uint32_t* slow_list;           // [n]
     uint32_t* slow_slot;           // [n]
     uint32_t* slow_buf;            // [n][SLOW_WORDS]
-    uint32_t* pbuf;                // [30][n] SoA, processing order: P = s B - h A (X, Y, Z rows)
+    uint32_t* pbuf;                // [PREC_ROWS][n] SoA, processing order: P's X, Z + partial flags
     uint32_t* pre;                 // [10][n] SoA prefix products of Z (k_finish scratch)
     const uint32_t* perm;          // [n] processing order for k_verify (signer-grouped) or null
 };

@@ -19,69 +19,17 @@
 #include <hip/hip_runtime.h>
 #include "nw_point.h"
 #include "nw_sha512.h"
-#include "nw_chacha.h"
 #include "nw_kernels.h"
 #include "nw_core.h"
 
 namespace nw {
 
-// Signature i's inputs and h = SHA-512(R || A || M) mod l.
-template <int MSGMODE>
-__device__ __forceinline__ void lane_inputs(const VerifyParams& a, uint32_t i, uint32_t R[8], uint32_t S[8],
-                                            uint32_t& slot, uint32_t& kinfo, uint32_t& cert, uint32_t h[8]) {
-    uint32_t Aw[8];
-    load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
-    load_w8(S, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16 + 8);
-    slot = a.signer[i];
-    load_w8(Aw, a.keys_raw + (size_t)slot * 8);
-    kinfo = a.key_info[slot];
-    cert = a.sig_cert[i];
-    if (MSGMODE == 0) {
-        uint32_t M[8];
-        load_w8(M, reinterpret_cast<const uint32_t*>(a.cert_msg) + (size_t)cert * 8);
-        hram_msg32(h, R, Aw, M);
-    } else {
-        uint32_t hw[16];
-        hram_generic(hw, R, Aw, a.msg_base + a.msg_off[i], a.msg_len[i]);
-        sc_reduce512(h, hw);
-    }
-}
-
-__device__ __forceinline__ void coeff_z(const VerifyParams& a, uint32_t i, uint32_t cert, uint32_t z4[4]) {
-    const uint64_t bidx = a.cert_base + cert;
-    chacha20_z(z4, a.zseed, i - a.cert_first[cert], (uint32_t)bidx, (uint32_t)(bidx >> 32), 0u);
-}
-
-// ------------------------------------------------------------------------------------ verify (P_i)
-// One lane per signature: P_i = s_i B - h_i A_i, written as (X, Y, Z) to pbuf; partial flags
-// (S ok, A ok, A small, torsion coefficient for torsion keys).
-#ifdef NW_VERIFY_WAVES
-#define NW_VERIFY_BOUNDS __launch_bounds__(256, NW_VERIFY_WAVES)
-#else
-#define NW_VERIFY_BOUNDS __launch_bounds__(256)
-#endif
-template <int MSGMODE, int WA>
-__global__ void NW_VERIFY_BOUNDS k_verify(VerifyParams a) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= a.n) return;
-    // signer-grouped order: the 64 lanes of a wave mostly share one key table (TLB / cache locality)
-    const uint32_t i = a.perm ? a.perm[gid] : gid;
-    uint32_t R[8], S[8], h[8], slot, kinfo, cert;
-    lane_inputs<MSGMODE>(a, i, R, S, slot, kinfo, cert, h);
-    const bool sok = sc_is_canonical(S);
-    const bool aok = (kinfo & KI_OK) != 0;
-    uint32_t flags = (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | ((kinfo & KI_SMALL) ? NW_F_A_SMALL : 0u);
-    const uint32_t tk = (kinfo >> KI_TORSION_SHIFT) & 7u;
-    if (a.batch_mode && tk != 0 && sok && aok) {   // torsion keys only (never for honest committees)
-        uint32_t z4[4];
-        coeff_z(a, i, cert, z4);
-        flags |= torsion_coef(z4, h, tk) << NW_F_TCOEF_SHIFT;
-    }
-    a.flags[i] = flags;
-    const ge_p3 P = compute_P<WA>(S, h, sok, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
-    // P in processing order, struct-of-arrays (column gid): coalesced for k_finish
-    store_xyz_soa(a.pbuf, a.n, gid, P);
-}
+template <int WA>
+hipError_t launch_vs_wa(const VerifyParams& p, int msgmode, bool slow, uint32_t n_upper, hipStream_t st);
+extern template hipError_t launch_vs_wa<8>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
+extern template hipError_t launch_vs_wa<12>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
+extern template hipError_t launch_vs_wa<16>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
+extern template hipError_t launch_vs_wa<20>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
 
 // ------------------------------------------------------------------------------------ signer grouping
 // Counting sort of signature indices by key-cache slot: perm lists the signatures of slot 0, then
@@ -172,20 +120,22 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
 // mismatching signatures into the exact-path list.  Lane L of NL owns the processing-order columns
 // g = L, L + NL, L + 2 NL, ... so every pbuf / pre access of a wave is one contiguous 256-B run.
 __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
-    const uint32_t NL = (a.n + FINISH_K - 1) / FINISH_K;
+    const uint32_t NL = (a.gn + a.fk - 1) / a.fk;
     const uint32_t L = blockIdx.x * blockDim.x + threadIdx.x;
     if (L >= NL) return;
-    const uint32_t cnt = (a.n - L + NL - 1) / NL;   // columns L + k NL < n
+    const uint32_t cnt = (a.gn - L + NL - 1) / NL;   // columns g0 + L + k NL < g0 + gn  (cnt <= fk)
     const size_t n = a.n;
+    const size_t gbase = (size_t)a.g0 + L;
     // Both chains are fully unrolled over FINISH_K (guarded by cnt) so the column loads are
     // independent of the running products and issue ahead of them: with one wave per SIMD the
     // kernel is latency-bound, and a load inside the serial chain would stall it every step.
+    const uint32_t* zrow = a.pbuf + 10 * n;
     fe acc = fe_one();
 #pragma unroll
     for (int k = 0; k < FINISH_K; ++k) {
         if ((uint32_t)k < cnt) {
-            const size_t g = L + (size_t)k * NL;
-            acc = fe_mul(acc, load_fe_soa(a.pbuf + 20 * n, n, g));
+            const size_t g = gbase + (size_t)k * NL;
+            acc = fe_mul(acc, load_fe_soa(zrow, n, g));
             store_fe_soa(a.pre, n, g, acc);
         }
     }
@@ -193,17 +143,14 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
 #pragma unroll
     for (int k = FINISH_K - 1; k >= 0; --k) {
         if ((uint32_t)k < cnt) {
-            const size_t g = L + (size_t)k * NL;
+            const size_t g = gbase + (size_t)k * NL;
             fe zi = inv;
             if (k > 0) {
                 zi = fe_mul(inv, load_fe_soa(a.pre, n, g - NL));
-                inv = fe_mul(inv, load_fe_soa(a.pbuf + 20 * n, n, g));
+                inv = fe_mul(inv, load_fe_soa(zrow, n, g));
             }
             const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
-            uint32_t R[8];
-            load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
-            uint32_t f = finish_flags(load_fe_soa(a.pbuf, n, g), load_fe_soa(a.pbuf + 10 * n, n, g), zi, R,
-                                      a.flags[i]);
+            uint32_t f = finish_x_flags(load_fe_soa(a.pbuf, n, g), zi, a.pbuf[PREC_FLAGS_ROW * n + g]);
             if (a.batch_mode && (f & (NW_F_S_OK | NW_F_A_OK)) == (NW_F_S_OK | NW_F_A_OK) && !(f & NW_F_MATCH)) {
                 f |= NW_F_SLOW;
                 const uint32_t t = atomicAdd(a.slow_count, 1u);
@@ -213,27 +160,6 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
             a.flags[i] = f;
         }
     }
-}
-
-// Exact path for signatures with D_i != O: Q_i = z_i (R_i - P_i); R decode failure -> F_R_BAD.
-template <int MSGMODE, int WA>
-__global__ void __launch_bounds__(256) k_slow_sig(VerifyParams a) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= *a.slow_count) return;
-    const uint32_t i = a.slow_list[t];
-    uint32_t* buf = a.slow_buf + (size_t)t * SLOW_WORDS;
-    uint32_t R[8], S[8], h[8], slot, kinfo, cert;
-    lane_inputs<MSGMODE>(a, i, R, S, slot, kinfo, cert, h);
-    ge_p3 Rp;
-    if (!ge_decompress(Rp, R)) {
-        a.flags[i] |= NW_F_R_BAD;
-        store_p3(buf, ge_identity());
-        return;
-    }
-    const ge_p3 P = compute_P<WA>(S, h, true, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
-    uint32_t z4[4];
-    coeff_z(a, i, cert, z4);
-    store_p3(buf, slow_term(Rp, P, z4));
 }
 
 // Per-certificate verdict: definitive Err on any bad S / undecodable A / undecodable R, else the
@@ -298,32 +224,6 @@ __global__ void __launch_bounds__(256) k_flags_to_ok(uint32_t n, const uint32_t*
     if (i < n) ok[i] = (flags[i] & NW_F_STRICT) ? 1 : 0;
 }
 
-// ------------------------------------------------------------------------------------ key cache
-// One thread per key: decode, small-order flag, torsion index, comb bases 2^(W i) A.
-template <int W>
-__global__ void __launch_bounds__(64) k_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info,
-                                                 uint32_t* bases) {
-    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nk) return;
-    key_info[j] = key_prep_one<W>(keys_raw + (size_t)j * 8, bases + (size_t)j * comb_pos(W) * 40);
-}
-
-// One thread per (key, position, chunk of COMB_CH entries): consecutive multiples with one batched
-// inversion per chunk (comb_chunk_build).
-static constexpr int COMB_CH = 8;
-
-template <int W>
-__global__ void __launch_bounds__(256) k_comb_build(uint32_t nk, const uint32_t* bases, uint32_t* tab) {
-    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t nch = (comb_ent(W) + COMB_CH - 1) / COMB_CH;
-    const uint64_t per_key = (uint64_t)comb_pos(W) * nch;
-    if (gid >= (uint64_t)nk * per_key) return;
-    const uint32_t j = (uint32_t)(gid / per_key);
-    const uint64_t rem = gid % per_key;
-    comb_chunk_build<W, COMB_CH>(bases + (size_t)j * comb_pos(W) * 40, (uint32_t)(rem / nch), (uint32_t)(rem % nch),
-                                 tab + (size_t)j * comb_words(W));
-}
-
 // ------------------------------------------------------------------------------------ SHA-512 bulk
 // One lane per message (each message is an inherently sequential compression chain).
 __global__ void __launch_bounds__(256) k_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off,
@@ -383,64 +283,26 @@ __global__ void __launch_bounds__(256) k_sha512_many(uint32_t n, const uint8_t* 
     for (int k = 0; k < 4; ++k) o[k] = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
 }
 
-// ------------------------------------------------------------------------------------ signing
-template <int MW>
-__global__ void __launch_bounds__(256) k_sign(uint32_t n, const uint32_t* seeds, const uint32_t* msgs,
-                                              const uint32_t* btab, uint32_t* pk_out, uint32_t* sig_out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint32_t pk[8], sig[16];
-    sign_one<MW>(seeds + (size_t)i * 8, msgs + (size_t)i * MW, btab, pk, sig);
-    if (pk_out) {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) pk_out[(size_t)i * 8 + k] = pk[k];
-    }
-    if (sig_out) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) sig_out[(size_t)i * 16 + k] = sig[k];
-    }
-}
-
 // ------------------------------------------------------------------------------------ launchers
-static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
-
-template <int MSGMODE>
-static void launch_verify_w(const VerifyParams& p, int wa, bool slow, uint32_t n_upper, hipStream_t st) {
-    const dim3 b(256);
-    const dim3 g(blocks_for(slow ? n_upper : p.n, 256));
-    switch (wa) {
-        case 8:
-            if (slow) hipLaunchKernelGGL((k_slow_sig<MSGMODE, 8>), g, b, 0, st, p);
-            else hipLaunchKernelGGL((k_verify<MSGMODE, 8>), g, b, 0, st, p);
-            break;
-        case 12:
-            if (slow) hipLaunchKernelGGL((k_slow_sig<MSGMODE, 12>), g, b, 0, st, p);
-            else hipLaunchKernelGGL((k_verify<MSGMODE, 12>), g, b, 0, st, p);
-            break;
-        case 16:
-            if (slow) hipLaunchKernelGGL((k_slow_sig<MSGMODE, 16>), g, b, 0, st, p);
-            else hipLaunchKernelGGL((k_verify<MSGMODE, 16>), g, b, 0, st, p);
-            break;
-        default:
-            if (slow) hipLaunchKernelGGL((k_slow_sig<MSGMODE, 20>), g, b, 0, st, p);
-            else hipLaunchKernelGGL((k_verify<MSGMODE, 20>), g, b, 0, st, p);
-            break;
-    }
-}
-
 static hipError_t launch_vs(const VerifyParams& p, int msgmode, int key_window, bool slow, uint32_t n_upper,
                             hipStream_t st) {
-    if (key_window != 8 && key_window != 12 && key_window != 16 && key_window != 20) return hipErrorInvalidValue;
-    if (msgmode == 0)
-        launch_verify_w<0>(p, key_window, slow, n_upper, st);
-    else
-        launch_verify_w<1>(p, key_window, slow, n_upper, st);
-    return hipGetLastError();
+    switch (key_window) {
+        case 8: return launch_vs_wa<8>(p, msgmode, slow, n_upper, st);
+        case 12: return launch_vs_wa<12>(p, msgmode, slow, n_upper, st);
+        case 16: return launch_vs_wa<16>(p, msgmode, slow, n_upper, st);
+        case 20: return launch_vs_wa<20>(p, msgmode, slow, n_upper, st);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_verify(const VerifyParams& p, int msgmode, int key_window, hipStream_t st) {
-    if (p.n == 0) return hipSuccess;
+    if (p.gn == 0) return hipSuccess;
     return launch_vs(p, msgmode, key_window, false, 0, st);
+}
+
+hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st) {
+    if (n_upper == 0) return hipSuccess;
+    return launch_vs(p, msgmode, key_window, true, n_upper, st);
 }
 
 hipError_t launch_group_by_signer(uint32_t n, uint32_t nkeys, const uint32_t* signer, uint32_t* counts,
@@ -464,15 +326,11 @@ hipError_t launch_group_by_signer(uint32_t n, uint32_t nkeys, const uint32_t* si
 }
 
 hipError_t launch_finish(const VerifyParams& p, hipStream_t st) {
-    if (p.n == 0) return hipSuccess;
-    const uint64_t lanes = (p.n + FINISH_K - 1) / FINISH_K;
+    if (p.gn == 0) return hipSuccess;
+    if (p.fk < 1 || p.fk > (uint32_t)FINISH_K || (uint64_t)p.g0 + p.gn > p.n) return hipErrorInvalidValue;
+    const uint64_t lanes = (p.gn + p.fk - 1) / p.fk;
     hipLaunchKernelGGL(k_finish, dim3(blocks_for(lanes, 256)), dim3(256), 0, st, p);
     return hipGetLastError();
-}
-
-hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st) {
-    if (n_upper == 0) return hipSuccess;
-    return launch_vs(p, msgmode, key_window, true, n_upper, st);
 }
 
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
@@ -495,46 +353,10 @@ hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hi
     return hipGetLastError();
 }
 
-template <int W>
-static hipError_t launch_key_prep_w(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
-                                    uint32_t* tab, hipStream_t st) {
-    hipLaunchKernelGGL(k_key_prep<W>, dim3(blocks_for(nk, 64)), dim3(64), 0, st, nk, keys_raw, key_info, bases);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const uint64_t total = (uint64_t)nk * comb_pos(W) * ((comb_ent(W) + COMB_CH - 1) / COMB_CH);
-    hipLaunchKernelGGL(k_comb_build<W>, dim3(blocks_for(total, 256)), dim3(256), 0, st, nk, bases, tab);
-    return hipGetLastError();
-}
-
-hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
-                           uint32_t* tab, int window, hipStream_t st) {
-    if (nk == 0) return hipSuccess;
-    switch (window) {
-        case 8: return launch_key_prep_w<8>(nk, keys_raw, key_info, bases, tab, st);
-        case 12: return launch_key_prep_w<12>(nk, keys_raw, key_info, bases, tab, st);
-        case 16: return launch_key_prep_w<16>(nk, keys_raw, key_info, bases, tab, st);
-        case 20: return launch_key_prep_w<20>(nk, keys_raw, key_info, bases, tab, st);
-        case B_WINDOW: return launch_key_prep_w<B_WINDOW>(nk, keys_raw, key_info, bases, tab, st);
-        default: return hipErrorInvalidValue;
-    }
-}
-
 hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                               uint8_t* out, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_sha512_many, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, base, off, len, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_sign(uint32_t n, int msg_words, const uint32_t* seeds, const uint32_t* msgs,
-                       const uint32_t* btab, uint32_t* pk, uint32_t* sig, hipStream_t st) {
-    if (n == 0) return hipSuccess;
-    if (msg_words == 8)
-        hipLaunchKernelGGL(k_sign<8>, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, seeds, msgs, btab, pk, sig);
-    else if (msg_words == 2)
-        hipLaunchKernelGGL(k_sign<2>, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, seeds, msgs, btab, pk, sig);
-    else
-        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
