@@ -31,7 +31,7 @@ METRIC = "Ed25519 sigs verified/s (node, 1/2/4/8 GPU); p50 latency per 2f+1 cert
 # kernel runs a different (cheaper) algorithm, so v1 is not its work.
 COST_MODEL_V1_FM = {3: 1750, 67: 1030, 667: 811, 977: 775, 6667: 644}
 MADS_PER_FM = 100          # 10 x 10 radix-2^25.5 limb products per field multiplication
-B_WINDOW = 24              # basepoint comb window (nw_point.h)
+B_WINDOW = 24              # default basepoint comb window (nw_point.h; the library reports its own)
 MADD_FM = 7                # mixed (affine Niels) addition = 7 field multiplications
 
 
@@ -39,11 +39,11 @@ def comb_pos(w):
     return (256 + w - 1) // w
 
 
-def kverify_fm_per_sig(key_window):
+def kverify_fm_per_sig(key_window, base_window=B_WINDOW):
     """k_verify's field multiplications per signature: one mixed addition per comb digit position
     of s (basepoint comb) and of h (key comb); no doublings (nw_core.h comb_sB_minus_hA).  The
     SHA-512 block, mod-l reduction and digit recoding are VALU work not counted here."""
-    return MADD_FM * (comb_pos(B_WINDOW) + comb_pos(key_window))
+    return MADD_FM * (comb_pos(base_window) + comb_pos(key_window))
 
 
 def valu_peak_mad_per_s():
@@ -255,7 +255,8 @@ def main():
             ksigs = cs.nsigs * kn
         sigs_per_launch = ksigs / kn if kn else 0.0
         kw = eng.key_window()
-        fm = kverify_fm_per_sig(kw)
+        bw = eng.base_window()
+        fm = kverify_fm_per_sig(kw, bw)
         peak = valu_peak_mad_per_s() / 1e12
         achieved = sigs_per_launch * fm * MADS_PER_FM / avg_launch_s / 1e12
         v1 = COST_MODEL_V1_FM.get(args.votes)
@@ -266,7 +267,7 @@ def main():
             "work_model": "%.0f sigs/launch (%d launches per step) x %d FM/sig (7 FM per mixed addition x (%d basepoint "
                           "+ %d key) comb positions, key window %d) x 100 u32 MADs; SHA-512/mod-l/recoding VALU work "
                           "not counted; peak = measured v_mad_u64_u32 rate"
-                          % (sigs_per_launch, kn // args.steps, fm, comb_pos(B_WINDOW), comb_pos(kw), kw),
+                          % (sigs_per_launch, kn // args.steps, fm, comb_pos(bw), comb_pos(kw), kw),
             "dalek_equiv": {"fm_per_sig": v1, "TMADps": (sigs_per_launch * v1 * MADS_PER_FM / avg_launch_s / 1e12)
                             if v1 else None,
                             "note": "SURVEY §8(d) cost model v1 = dalek's MSM work per signature; the comb "

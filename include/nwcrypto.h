@@ -80,6 +80,8 @@ int nw_committee_load(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stak
 size_t nw_committee_size(const nw_ctx* ctx);
 /* Key comb window in use (8 / 12 / 16; 0 before the first load). */
 int nw_key_window(const nw_ctx* ctx);
+/* Basepoint comb window this library was built with (additions per s*B = ceil(256 / w)). */
+int nw_base_window(void);
 
 /* ---- verification ----------------------------------------------------------------------------
  * crypto::Signature::verify (crypto/src/lib.rs:200-204): strict single verify of ``msg``. */
@@ -156,6 +158,71 @@ int nw_profile_read(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launc
 /* Same, plus the signatures covered by those launches (the roofline's work per launch). */
 int nw_profile_read_sigs(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launches,
                          uint64_t* verify_sigs);
+
+/* ---- primary certificate path -------------------------------------
+ * Native ingestion of bincode ``PrimaryMessage`` frames (primary/src/primary.rs:236) and the whole
+ * of Certificate::verify (primary/src/messages.rs:189-215, Header::verify :48-67) for many
+ * certificates: host checks in C++, all crypto on the GPU in three submissions.  Verdicts are the
+ * DagError kinds the reference returns (primary/src/error.rs:24-58), checked in its order. */
+#define NW_DAG_PENDING (-1)             /* decode only: needs the GPU checks */
+#define NW_DAG_OK 0
+#define NW_DAG_INVALID_SIGNATURE 1      /* DagError::InvalidSignature */
+#define NW_DAG_SERIALIZATION 2          /* DagError::SerializationError (bincode / base64 key) */
+#define NW_DAG_INVALID_HEADER_ID 3      /* DagError::InvalidHeaderId */
+#define NW_DAG_MALFORMED_HEADER 4       /* DagError::MalformedHeader */
+#define NW_DAG_UNKNOWN_AUTHORITY 5      /* DagError::UnknownAuthority */
+#define NW_DAG_AUTHORITY_REUSE 6        /* DagError::AuthorityReuse */
+#define NW_DAG_REQUIRES_QUORUM 7        /* DagError::CertificateRequiresQuorum */
+#define NW_DAG_NOT_CERTIFICATE 8        /* a valid PrimaryMessage variant other than Certificate */
+
+/* Committee (config/src/lib.rs:161-240): authority i is name[i] with stake[i]; its worker ids are
+ * worker_id[worker_first[i] .. worker_first[i + 1]) (worker_first has n + 1 entries; both NULL =
+ * no workers, so any header with a payload is MalformedHeader). */
+typedef struct nw_committee {
+    size_t n;
+    const uint8_t (*name)[32];
+    const uint32_t* stake;
+    const uint32_t* worker_first;
+    const uint32_t* worker_id;
+} nw_committee;
+
+typedef struct nw_cert_batch nw_cert_batch;
+
+/* Decoded view of one certificate of a batch.  Pointers stay valid until nw_cert_batch_free. */
+typedef struct nw_cert_view {
+    int32_t status;                  /* NW_DAG_PENDING, or a final verdict found while decoding
+                                        (SERIALIZATION, NOT_CERTIFICATE, OK for genesis) */
+    int32_t header_error;            /* Header::verify check after the id (UNKNOWN_AUTHORITY /
+                                        MALFORMED_HEADER) or NW_DAG_OK */
+    int32_t quorum_error;            /* quorum check (AUTHORITY_REUSE / UNKNOWN_AUTHORITY /
+                                        REQUIRES_QUORUM) or NW_DAG_OK */
+    uint64_t round;
+    const uint8_t* author;           /* 32 B */
+    const uint8_t* header_id;        /* 32 B */
+    const uint8_t* header_sig;       /* 64 B */
+    const uint8_t* header_preimage;  /* Hash for Header (primary/src/messages.rs:70-84) */
+    size_t header_preimage_len;
+    const uint8_t* cert_preimage;    /* 72 B: Hash for Certificate (:226-234) */
+    uint32_t first_vote, n_votes;
+    const uint8_t* vote_keys;        /* [n_votes][32] */
+    const uint8_t* vote_sigs;        /* [n_votes][64] */
+} nw_cert_view;
+
+/* Host only (no context, no GPU): decode n frames and run the host-side checks. */
+int nw_cert_batch_decode(const nw_committee* committee, const uint8_t* const* frame, const size_t* len,
+                         size_t n, nw_cert_batch** out);
+size_t nw_cert_batch_size(const nw_cert_batch* batch);
+int nw_cert_batch_view(const nw_cert_batch* batch, size_t i, nw_cert_view* out);
+void nw_cert_batch_free(nw_cert_batch* batch);
+/* The GPU half: header/certificate digests, header signatures, vote batches.  verdict[i] receives
+ * the NW_DAG_* verdict of certificate i.  Batch coefficients (NW-Z v1) use batch index cert_base + j
+ * for the j-th certificate that reaches the batch step. */
+int nw_cert_batch_verify(nw_ctx* ctx, const nw_cert_batch* batch, const uint8_t zseed[32],
+                         uint64_t cert_base, int32_t* verdict);
+/* decode + verify + free in one call. */
+int nw_certificates_verify(nw_ctx* ctx, const nw_committee* committee, const uint8_t* const* frame,
+                           const size_t* len, size_t n, const uint8_t zseed[32], uint64_t cert_base,
+                           int32_t* verdict);
 
 /* Library build identifier (gfx target, build date). */
 const char* nw_version(void);

@@ -33,7 +33,27 @@ class NwCert(ctypes.Structure):
     _fields_ = [("first_vote", ctypes.c_uint32), ("n_votes", ctypes.c_uint32)]
 
 
-_OPTIONAL = {"nw_profile_read_sigs"}
+class NwCommittee(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_size_t), ("name", ctypes.c_void_p), ("stake", ctypes.c_void_p),
+                ("worker_first", ctypes.c_void_p), ("worker_id", ctypes.c_void_p)]
+
+
+class NwCertView(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("header_error", ctypes.c_int32), ("quorum_error", ctypes.c_int32),
+                ("round", ctypes.c_uint64), ("author", ctypes.c_void_p), ("header_id", ctypes.c_void_p),
+                ("header_sig", ctypes.c_void_p), ("header_preimage", ctypes.c_void_p),
+                ("header_preimage_len", ctypes.c_size_t), ("cert_preimage", ctypes.c_void_p),
+                ("first_vote", ctypes.c_uint32), ("n_votes", ctypes.c_uint32), ("vote_keys", ctypes.c_void_p),
+                ("vote_sigs", ctypes.c_void_p)]
+
+
+# NW_DAG_* verdicts (include/nwcrypto.h; primary/src/error.rs DagError kinds)
+DAG_PENDING, DAG_OK, DAG_INVALID_SIGNATURE, DAG_SERIALIZATION, DAG_INVALID_HEADER_ID = -1, 0, 1, 2, 3
+DAG_MALFORMED_HEADER, DAG_UNKNOWN_AUTHORITY, DAG_AUTHORITY_REUSE, DAG_REQUIRES_QUORUM = 4, 5, 6, 7
+DAG_NOT_CERTIFICATE = 8
+
+_OPTIONAL = {"nw_profile_read_sigs", "nw_base_window", "nw_cert_batch_decode", "nw_cert_batch_size",
+             "nw_cert_batch_view", "nw_cert_batch_free", "nw_cert_batch_verify", "nw_certificates_verify"}
 
 
 def _load() -> ctypes.CDLL:
@@ -49,6 +69,7 @@ def _load() -> ctypes.CDLL:
         "nw_committee_load": (I, [P, P, P, S, P]),
         "nw_committee_size": (S, [P]),
         "nw_key_window": (I, [P]),
+        "nw_base_window": (I, []),
         "nw_verify_strict": (I, [P, P, S, P, P]),
         "nw_verify_strict_many": (I, [P, P, P, P, P, S, P]),
         "nw_verify_batch": (I, [P, P, P, P, P, S, P, U64]),
@@ -64,6 +85,12 @@ def _load() -> ctypes.CDLL:
         "nw_profile_read": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]),
         "nw_profile_read_sigs": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "nw_version": (ctypes.c_char_p, []),
+        "nw_cert_batch_decode": (I, [ctypes.POINTER(NwCommittee), P, P, S, ctypes.POINTER(P)]),
+        "nw_cert_batch_size": (S, [P]),
+        "nw_cert_batch_view": (I, [P, S, ctypes.POINTER(NwCertView)]),
+        "nw_cert_batch_free": (None, [P]),
+        "nw_cert_batch_verify": (I, [P, P, P, U64, P]),
+        "nw_certificates_verify": (I, [P, ctypes.POINTER(NwCommittee), P, P, S, P, U64, P]),
     }
     for name, (res, args) in sig.items():
         if name in _OPTIONAL and not hasattr(lib, name):
@@ -132,6 +159,10 @@ class Engine:
 
     def key_window(self) -> int:
         return LIB.nw_key_window(self._ctx)
+
+    @staticmethod
+    def base_window() -> int:
+        return LIB.nw_base_window()
 
     # -- verification -------------------------------------------------------------------------
     def verify_strict(self, msg: bytes, pk: bytes, sig: bytes) -> bool:
@@ -316,6 +347,81 @@ class Engine:
 
     def sha512_many_dev(self, d_base, d_off, d_len, n, d_out, stream):
         self.check(LIB.nw_sha512_many_dev(self._ctx, d_base, d_off, d_len, n, d_out, stream), "nw_sha512_many_dev")
+
+    # -- primary certificate path (nw_cert_batch_verify) ----------------------------------------
+    def cert_batch_verify(self, batch: "CertBatch", zseed: bytes, cert_base: int = 0):
+        """NW_DAG_* verdict per certificate of a decoded batch (GPU: digests, header signatures,
+        vote batches)."""
+        n = len(batch)
+        out = (ctypes.c_int32 * max(n, 1))()
+        self.check(LIB.nw_cert_batch_verify(self._ctx, batch.handle, _buf(bytes(zseed)), cert_base, out),
+                   "nw_cert_batch_verify")
+        return list(out[:n])
+
+
+class CommitteeABI:
+    """nw_committee view of (names, stakes, worker id lists); keeps the buffers alive."""
+
+    def __init__(self, names, stakes, workers):
+        names = [bytes(k) for k in names]
+        n = len(names)
+        self._names = b"".join(names)
+        self._stake = (ctypes.c_uint32 * max(n, 1))(*stakes)
+        first, ids = [0], []
+        for ws in workers:
+            ids.extend(sorted(ws))
+            first.append(len(ids))
+        self._first = (ctypes.c_uint32 * len(first))(*first)
+        self._ids = (ctypes.c_uint32 * max(len(ids), 1))(*ids)
+        self.struct = NwCommittee(n, ctypes.cast(ctypes.c_char_p(self._names), ctypes.c_void_p) if n else None,
+                                  ctypes.cast(self._stake, ctypes.c_void_p), ctypes.cast(self._first, ctypes.c_void_p),
+                                  ctypes.cast(self._ids, ctypes.c_void_p))
+
+
+class CertBatch:
+    """Host-side decode of bincode PrimaryMessage frames (nw_cert_batch_decode: C++, no GPU)."""
+
+    def __init__(self, committee: CommitteeABI, frames):
+        frames = [bytes(f) for f in frames]
+        n = len(frames)
+        self._frames = frames
+        ptrs = (ctypes.c_char_p * max(n, 1))(*frames)
+        lens = (ctypes.c_size_t * max(n, 1))(*[len(f) for f in frames])
+        self._h = ctypes.c_void_p()
+        rc = LIB.nw_cert_batch_decode(ctypes.byref(committee.struct), ptrs, lens, n, ctypes.byref(self._h))
+        if rc != NW_OK:
+            raise DeviceError("nw_cert_batch_decode failed (rc=%d)" % rc)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __len__(self):
+        return LIB.nw_cert_batch_size(self._h)
+
+    def view(self, i: int) -> dict:
+        v = NwCertView()
+        if LIB.nw_cert_batch_view(self._h, i, ctypes.byref(v)) != NW_OK:
+            raise IndexError(i)
+
+        def rd(p, k):
+            return ctypes.string_at(p, k) if k else b""
+        return {"status": v.status, "header_error": v.header_error, "quorum_error": v.quorum_error,
+                "round": v.round, "author": rd(v.author, 32), "header_id": rd(v.header_id, 32),
+                "header_sig": rd(v.header_sig, 64), "header_preimage": rd(v.header_preimage, v.header_preimage_len),
+                "cert_preimage": rd(v.cert_preimage, 72),
+                "votes": [(rd(v.vote_keys + 32 * j, 32), rd(v.vote_sigs + 64 * j, 64)) for j in range(v.n_votes)]}
+
+    def close(self):
+        if self._h:
+            LIB.nw_cert_batch_free(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 _default: Optional[Engine] = None

@@ -515,6 +515,8 @@ size_t nw_committee_size(const nw_ctx* ctx) { return ctx ? ctx->nkeys : 0; }
 
 int nw_key_window(const nw_ctx* ctx) { return ctx ? ctx->key_window : 0; }
 
+int nw_base_window(void) { return B_WINDOW; }
+
 int nw_committee_load(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, size_t n, uint32_t* slot_out) {
     if (!ctx || (!pk && n)) return NW_ERR_ARG;
     std::lock_guard<std::mutex> g(ctx->mu);

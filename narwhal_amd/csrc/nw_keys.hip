@@ -65,12 +65,12 @@ static hipError_t launch_key_prep_w(uint32_t nk, const uint32_t* keys_raw, uint3
 hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
                            uint32_t* tab, int window, hipStream_t st) {
     if (nk == 0) return hipSuccess;
+    if (window == B_WINDOW) return launch_key_prep_w<B_WINDOW>(nk, keys_raw, key_info, bases, tab, st);
     switch (window) {
         case 8: return launch_key_prep_w<8>(nk, keys_raw, key_info, bases, tab, st);
         case 12: return launch_key_prep_w<12>(nk, keys_raw, key_info, bases, tab, st);
         case 16: return launch_key_prep_w<16>(nk, keys_raw, key_info, bases, tab, st);
         case 20: return launch_key_prep_w<20>(nk, keys_raw, key_info, bases, tab, st);
-        case B_WINDOW: return launch_key_prep_w<B_WINDOW>(nk, keys_raw, key_info, bases, tab, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -34,7 +34,10 @@ static constexpr int PRECOMP_WORDS = 32;
 NW_HD constexpr int comb_pos(int w) { return (256 + w - 1) / w; }
 NW_HD constexpr int comb_ent(int w) { return (1 << (w - 1)) + 1; }
 NW_HD constexpr size_t comb_words(int w) { return (size_t)comb_pos(w) * comb_ent(w) * PRECOMP_WORDS; }
-static constexpr int B_WINDOW = 24;
+#ifndef NW_BW
+#define NW_BW 24
+#endif
+static constexpr int B_WINDOW = NW_BW;
 
 NW_HD ge_p3 ge_identity() {
     ge_p3 r;

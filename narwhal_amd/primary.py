@@ -109,14 +109,36 @@ class _Reader:
 
     def public_key(self) -> bytes:
         """PublicKey serializes as its base64 string (crypto/src/lib.rs:94-112)."""
-        s = self.take(self.u64())
-        try:
-            raw = base64.b64decode(s, validate=True)
-        except Exception as e:  # noqa: BLE001
-            raise SerializationError("bad base64 public key") from e
+        raw = _b64_decode(self.take(self.u64()))
+        if raw is None:
+            raise SerializationError("bad base64 public key")
         if len(raw) < 32:
             raise SerializationError("public key too short")
         return raw[:32]
+
+
+_B64 = b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"
+
+
+def _b64_decode(s: bytes) -> Optional[bytes]:
+    """base64 0.13 STANDARD decode (crypto/src/lib.rs:73) as restated in nw_primary.cpp b64_decode:
+    '=' padding optional but, when present, only at the end completing the last quantum; a
+    1-symbol final quantum and non-zero trailing bits are rejected.  None = decode error."""
+    n = len(s)
+    pad = 0
+    while pad < min(n, 2) and s[n - 1 - pad:n - pad] == b"=":
+        pad += 1
+    m = n - pad
+    if (pad and n % 4) or m % 4 == 1 or (pad and m % 4 + pad != 4):
+        return None
+    if any(c not in _B64 for c in s[:m]):
+        return None
+    full = bytes(s[:m]) + b"=" * (-m % 4)
+    out = base64.b64decode(full)
+    # trailing bits of the last symbol must be zero (re-encoding reproduces the symbols)
+    if base64.b64encode(out)[:m] != bytes(s[:m]):
+        return None
+    return out
 
 
 def _pk_bytes(pk: bytes) -> bytes:
@@ -306,10 +328,8 @@ def decode_primary_message(buf: bytes):
     tag = r.u32()
     if tag not in _VARIANTS:
         raise SerializationError("unsupported PrimaryMessage variant %d" % tag)
-    msg = _VARIANTS[tag].read(r)
-    if r.p != len(buf):
-        raise SerializationError("trailing bytes")
-    return msg
+    # bincode::deserialize (bincode 1.3, primary/src/primary.rs:236) allows trailing bytes
+    return _VARIANTS[tag].read(r)
 
 
 # ----------------------------------------------------------------------------- bulk (Core batching)
@@ -398,3 +418,53 @@ def verify_certificates(certs: Sequence[Certificate], committee: Committee, engi
             if not good:
                 out[i] = InvalidSignature()
     return out
+
+
+# ----------------------------------------------------------------------------- native wire path
+class NotACertificate(DagError):
+    """A well-formed PrimaryMessage that is not a Certificate (the native certificate path only)."""
+
+
+_DAG_KIND = {
+    _lib.DAG_INVALID_SIGNATURE: InvalidSignature, _lib.DAG_SERIALIZATION: SerializationError,
+    _lib.DAG_INVALID_HEADER_ID: InvalidHeaderId, _lib.DAG_MALFORMED_HEADER: MalformedHeader,
+    _lib.DAG_UNKNOWN_AUTHORITY: UnknownAuthority, _lib.DAG_AUTHORITY_REUSE: AuthorityReuse,
+    _lib.DAG_REQUIRES_QUORUM: CertificateRequiresQuorum, _lib.DAG_NOT_CERTIFICATE: NotACertificate,
+}
+
+_abi_cache: Dict[int, Tuple[Committee, "_lib.CommitteeABI"]] = {}
+
+
+def committee_abi(committee: Committee) -> "_lib.CommitteeABI":
+    """nw_committee view of a Committee (BTreeMap order, as nw_committee_load gets it)."""
+    hit = _abi_cache.get(id(committee))
+    if hit is None or hit[0] is not committee:
+        keys = committee.keys()
+        abi = _lib.CommitteeABI(keys, [committee.stake(k) for k in keys],
+                                [committee.authorities[k][1] for k in keys])
+        hit = _abi_cache[id(committee)] = (committee, abi)
+    return hit[1]
+
+
+def decode_certificate_frames(frames: Sequence[bytes], committee: Committee) -> "_lib.CertBatch":
+    """Native (C++) bincode decode + host checks of many PrimaryMessage frames (no GPU)."""
+    return _lib.CertBatch(committee_abi(committee), frames)
+
+
+def verify_certificate_frames(frames: Sequence[bytes], committee: Committee, engine=None,
+                              zseed: Optional[bytes] = None, cert_base: int = 0) -> List[Optional[DagError]]:
+    """What the primary does with each received ``PrimaryMessage::Certificate`` frame
+    (primary/src/primary.rs:236 deserialize, then Certificate::verify, messages.rs:189-215), for many
+    frames at once on the native path: C++ decode into SoA, then three GPU submissions.  Returns
+    None (Ok) or the DagError per frame; same verdicts and coefficient indexing as
+    ``verify_certificates`` over the decoded certificates."""
+    import os
+    eng = engine or _lib.default_engine()
+    if zseed is None:
+        zseed = os.urandom(32)
+    batch = decode_certificate_frames(frames, committee)
+    try:
+        codes = eng.cert_batch_verify(batch, zseed, cert_base)
+    finally:
+        batch.close()
+    return [None if c == _lib.DAG_OK else _DAG_KIND[c]() for c in codes]

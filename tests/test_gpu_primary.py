@@ -93,6 +93,13 @@ def test_error_kinds(engine, world):
                 cert.verify(com, engine)
     got = pm.verify_certificates([c for c, _ in cases], com, engine)
     assert [type(e) if e else None for e in got] == [w for _, w in cases]
+    # the native wire path (C++ bincode decode + the same three GPU submissions) on the frames
+    frames = [pm.encode_primary_message(c) for c, _ in cases]
+    frames.append(frames[-1][:-3])                                               # truncated
+    frames.append(pm.encode_primary_message(pm.Vote(h.id, 1, h.author, keys[0])))  # not a certificate
+    native = pm.verify_certificate_frames(frames, com, engine)
+    assert [type(e) if e else None for e in native] == [w for _, w in cases] + [pm.SerializationError,
+                                                                               pm.NotACertificate]
 
 
 def test_bulk_matches_oracle(engine, world):
@@ -114,3 +121,41 @@ def test_bulk_matches_oracle(engine, world):
         want = o.crypto_verify_batch(o.digest32(c.digest_preimage()), c.votes, zseed, 100 + j)
         assert (got[j] is None) == want, j
         assert (got[j] is None) == (j % 5 != 2)
+    # native wire path: same verdicts and coefficient indexing from the bincode frames
+    native = pm.verify_certificate_frames([pm.encode_primary_message(c) for c in certs], com, engine,
+                                          zseed=zseed, cert_base=100)
+    assert [type(e) if e else None for e in native] == [type(e) if e else None for e in got]
+
+
+def test_native_frames_committee_scale(engine):
+    """Native path at a 100-validator committee (C2 shape, 67-vote certificates): honest frames
+    accepted, one corrupted vote signature rejected, against the oracle's batch verdict."""
+    from narwhal_amd import _lib
+    rng = random.Random(5)
+    seeds = [bytes([i + 1]) * 32 for i in range(100)]
+    keys, _ = engine.sign_many(seeds, [bytes(32)] * 100)
+    com = pm.Committee({k: (1, [0]) for k in keys})
+    assert com.quorum_threshold() == 67
+    order = sorted(range(100), key=lambda i: keys[i])
+    certs = []
+    for r in range(24):
+        a = order[r % 100]
+        h = pm.Header(keys[a], r + 1, {rng.randbytes(32): 0}, [rng.randbytes(32) for _ in range(67)])
+        h.id = o.digest32(h.digest_preimage())
+        h.signature = o.sign(seeds[a], h.id)
+        voters = rng.sample(range(100), 67)
+        v = pm.Vote(h.id, h.round, h.author, keys[0])
+        d = o.digest32(v.digest_preimage())
+        _, sigs = engine.sign_many([seeds[i] for i in voters], [d] * 67)
+        c = pm.Certificate(h, [(keys[i], s) for i, s in zip(voters, sigs)])
+        if r % 6 == 5:
+            k, s = c.votes[30]
+            c.votes[30] = (k, s[:5] + bytes([s[5] ^ 1]) + s[6:])
+        certs.append(c)
+    zseed = bytes([7]) * 32
+    native = pm.verify_certificate_frames([pm.encode_primary_message(c) for c in certs], com, engine,
+                                          zseed=zseed, cert_base=0)
+    for j, c in enumerate(certs):
+        want = o.crypto_verify_batch(o.digest32(c.digest_preimage()), c.votes, zseed, j)
+        assert (native[j] is None) == want == (j % 6 != 5), j
+    assert _lib.DAG_OK == 0
