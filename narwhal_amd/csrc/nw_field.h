@@ -301,12 +301,38 @@ NW_HD bool fe_eq(const fe& f, const fe& g) {
     return fe_iszero(fe_sub(f, g));
 }
 
-NW_HD fe fe_select(const fe& a, const fe& b, bool take_b) {
+// All-ones / zero lane mask from a predicate.  On the device the mask is hidden from the optimizer
+// so that the xor/and selects below stay bit operations (v_bfi_b32 / v_bitop3_b32) instead of
+// being recognised as selects and lowered to v_cndmask_b32 (a dependent chain of which issues at
+// 11 cycles per wave64 instruction on gfx950, profiles/r01/isa/isa_rates_vop2.jsonl).  A/B on
+// MI355X at C2 (profiles/r01_ab_select.txt): k_verify 1.214 ms vs 1.230 ms with cndmask selects.
+NW_HD uint32_t lane_mask(bool b) {
+    uint32_t m = 0u - (uint32_t)b;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(NW_CNDMASK_SELECT)
+    asm("" : "+v"(m));
+#endif
+    return m;
+}
+
+NW_HD fe fe_select_mask(const fe& a, const fe& b, uint32_t m) {
     fe r;
-    const uint32_t m = take_b ? 0xFFFFFFFFu : 0u;
 #pragma unroll
     for (int i = 0; i < 10; ++i) r.v[i] = a.v[i] ^ ((a.v[i] ^ b.v[i]) & m);
     return r;
+}
+
+NW_HD fe fe_select(const fe& a, const fe& b, bool take_b) {
+    return fe_select_mask(a, b, lane_mask(take_b));
+}
+
+// (a, b) <- (b, a) where m is all-ones: 3 bit operations per limb pair.
+NW_HD void fe_cswap_mask(fe& a, fe& b, uint32_t m) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        const uint32_t t = (a.v[i] ^ b.v[i]) & m;
+        a.v[i] ^= t;
+        b.v[i] ^= t;
+    }
 }
 
 // curve25519-dalek FieldElement::sqrt_ratio_i (see oracle/ed25519_oracle.py sqrt_ratio_i).

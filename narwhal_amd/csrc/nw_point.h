@@ -215,10 +215,10 @@ NW_HD bool y_is_small_order(const uint32_t yw[8]) {
 
 // Conditionally negate an affine Niels entry: -(x, y) = (-x, y) swaps y+x / y-x and negates 2dxy.
 NW_HD ge_precomp ge_precomp_cneg(const ge_precomp& q, bool neg) {
-    ge_precomp r;
-    r.ypx = fe_select(q.ypx, q.ymx, neg);
-    r.ymx = fe_select(q.ymx, q.ypx, neg);
-    r.xy2d = fe_select(q.xy2d, fe_neg(q.xy2d), neg);   // k <= 2
+    ge_precomp r = q;
+    const uint32_t m = lane_mask(neg);
+    fe_cswap_mask(r.ypx, r.ymx, m);
+    r.xy2d = fe_select_mask(q.xy2d, fe_neg(q.xy2d), m);   // k <= 2
     return r;
 }
 
