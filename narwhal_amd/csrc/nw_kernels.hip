@@ -237,13 +237,27 @@ __global__ void __launch_bounds__(256) k_sha512_many(uint32_t n, const uint8_t* 
     sha512_init(st);
     uint64_t w[16];
     const bool aligned = (reinterpret_cast<uintptr_t>(m) & 3u) == 0;
-    for (uint64_t b = 0; b < nfull; ++b) {
-        const uint8_t* blk = m + b * 128;
-        if (aligned) {
-            const uint32_t* p = reinterpret_cast<const uint32_t*>(blk);
+    if (aligned && nfull) {
+        // One wave per SIMD at worker-batch counts: nothing else hides the load latency, so the
+        // next block's 32 words are loaded before the current block is compressed.
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(m);
+        uint32_t nx[32];
 #pragma unroll
-            for (int k = 0; k < 16; ++k) w[k] = be64_from_le32(p[2 * k], p[2 * k + 1]);
-        } else {
+        for (int k = 0; k < 32; ++k) nx[k] = p[k];
+        for (uint64_t b = 0; b < nfull; ++b) {
+#pragma unroll
+            for (int k = 0; k < 16; ++k) w[k] = be64_from_le32(nx[2 * k], nx[2 * k + 1]);
+            if (b + 1 < nfull) {
+                const uint32_t* q = p + (b + 1) * 32;
+#pragma unroll
+                for (int k = 0; k < 32; ++k) nx[k] = q[k];
+            }
+            sha512_compress(st, w);
+        }
+    }
+    for (uint64_t b = 0; !aligned && b < nfull; ++b) {
+        const uint8_t* blk = m + b * 128;
+        {
 #pragma unroll
             for (int k = 0; k < 16; ++k) {
                 uint64_t x = 0;

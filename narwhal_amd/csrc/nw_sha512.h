@@ -37,9 +37,53 @@ static constexpr uint64_t SHA512_IV[8] = {
     0x6a09e667f3bcc908ull, 0xbb67ae8584caa73bull, 0x3c6ef372fe94f82bull, 0xa54ff53a5f1d36f1ull,
     0x510e527fade682d1ull, 0x9b05688c2b3e6c1full, 0x1f83d9abfb41bd6bull, 0x5be0cd19137e2179ull};
 
-NW_HD uint64_t rotr64(uint64_t x, int n) { return __builtin_rotateright64(x, n); }
+// 64-bit rotate as two funnel shifts (v_alignbit_b32) on the device: the generic rotate lowers to
+// v_lshrrev_b64 + v_lshlrev_b64 + 2 x v_or_b32, twice the instructions.  n is a compile-time
+// constant at every call site, so the half swap for n >= 32 folds away.
+NW_HD uint64_t rotr64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if (n >= 32) {
+        const uint32_t t = lo;
+        lo = hi;
+        hi = t;
+        n -= 32;
+    }
+    const uint32_t rlo = __builtin_amdgcn_alignbit(hi, lo, (uint32_t)n);
+    const uint32_t rhi = __builtin_amdgcn_alignbit(lo, hi, (uint32_t)n);
+    return ((uint64_t)rhi << 32) | rlo;
+#else
+    return __builtin_rotateright64(x, n);
+#endif
+}
 
 NW_HD uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// Three-input bit functions as one gfx950 v_bitop3_b32 per 32-bit half (truth table over
+// S0 = 0xF0, S1 = 0xCC, S2 = 0xAA): the compiler emits two or three 2-input ops per half for them.
+template <int TT>
+NW_HD uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint32_t lo, hi;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4"
+        : "=v"(lo) : "v"((uint32_t)a), "v"((uint32_t)b), "v"((uint32_t)c), "i"(TT));
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4"
+        : "=v"(hi) : "v"((uint32_t)(a >> 32)), "v"((uint32_t)(b >> 32)), "v"((uint32_t)(c >> 32)), "i"(TT));
+    return ((uint64_t)hi << 32) | lo;
+#else
+    uint64_t r = 0;
+    for (int bit = 0; bit < 64; ++bit) {
+        const int idx = (int)(((a >> bit) & 1) << 2 | ((b >> bit) & 1) << 1 | ((c >> bit) & 1));
+        r |= (uint64_t)((TT >> idx) & 1) << bit;
+    }
+    return r;
+#endif
+}
+
+NW_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0x96>(a, b, c); }
+
+// Maj(a, b, c) = (a & b) | (a & c) | (b & c)
+NW_HD uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0xE8>(a, b, c); }
 
 // big-endian 64-bit word from two little-endian-loaded u32 (bytes b0..b3 in lo, b4..b7 in hi)
 NW_HD uint64_t be64_from_le32(uint32_t lo, uint32_t hi) {
@@ -48,10 +92,10 @@ NW_HD uint64_t be64_from_le32(uint32_t lo, uint32_t hi) {
 
 #define NW_SHA_ROUND(a, b, c, d, e, f, g, h, k, w)                                        \
     do {                                                                                    \
-        const uint64_t t1 = (h) + (rotr64((e), 14) ^ rotr64((e), 18) ^ rotr64((e), 41)) +  \
+        const uint64_t t1 = (h) + xor3_64(rotr64((e), 14), rotr64((e), 18), rotr64((e), 41)) + \
                             (((e) & (f)) ^ (~(e) & (g))) + (k) + (w);                       \
-        const uint64_t t2 = (rotr64((a), 28) ^ rotr64((a), 34) ^ rotr64((a), 39)) +        \
-                            (((a) & (b)) ^ ((a) & (c)) ^ ((b) & (c)));                      \
+        const uint64_t t2 = xor3_64(rotr64((a), 28), rotr64((a), 34), rotr64((a), 39)) +   \
+                            maj64((a), (b), (c));                                           \
         (d) += t1;                                                                          \
         (h) = t1 + t2;                                                                      \
     } while (0)
@@ -68,8 +112,8 @@ NW_HD void sha512_compress(uint64_t st[8], const uint64_t win[16]) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-                const uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-                const uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
+                const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
+                const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
                 w[i] += s0 + w[(i + 9) & 15] + s1;
             }
         }
