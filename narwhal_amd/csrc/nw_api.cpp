@@ -43,6 +43,34 @@ struct DevBuf {
     }
 };
 
+// Pinned host staging buffer: one DMA per direction for the host-buffer entry points (pageable
+// hipMemcpyAsync stages every call through a driver bounce buffer synchronously).
+struct HostBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) {
+            hipError_t e = hipHostFree(p);
+            if (e != hipSuccess) return e;
+            p = nullptr;
+            cap = 0;
+        }
+        size_t want = bytes < 65536 ? 65536 : bytes + bytes / 4;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    uint8_t* bytes() const { return reinterpret_cast<uint8_t*>(p); }
+};
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 }  // namespace
 
 struct nw_ctx {
@@ -73,7 +101,8 @@ struct nw_ctx {
     // workspace
     DevBuf w_bases, w_sig, w_signer, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len,
         w_flags, w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_stake_out, w_ok, w_misc,
-        w_out, w_pbuf, w_pre, w_counts, w_cursor, w_perm;
+        w_out, w_pbuf, w_pre, w_counts, w_cursor, w_perm, w_io;
+    HostBuf h_io;
 };
 
 namespace {
@@ -466,8 +495,9 @@ void nw_ctx_destroy(nw_ctx* ctx) {
                       &ctx->w_msg, &ctx->w_msg_off, &ctx->w_msg_len, &ctx->w_flags, &ctx->w_slow_count,
                       &ctx->w_slow_list, &ctx->w_slow_slot, &ctx->w_slow_buf, &ctx->w_cert_ok, &ctx->w_stake_out,
                       &ctx->w_ok, &ctx->w_misc, &ctx->w_out, &ctx->w_pbuf, &ctx->w_pre,
-                      &ctx->w_counts, &ctx->w_cursor, &ctx->w_perm})
+                      &ctx->w_counts, &ctx->w_cursor, &ctx->w_perm, &ctx->w_io})
         b->release();
+    ctx->h_io.release();
     for (auto& ev : ctx->prof_events) {
         (void)hipEventDestroy(ev.first);
         (void)hipEventDestroy(ev.second);
@@ -578,38 +608,43 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
             ctx->last_error = "signer slot out of range (load the committee first)";
             return NW_ERR_ARG;
         }
-    NW_TRY(ctx->w_sig.ensure(nsigs * 64 + 64), "ws sig");
-    NW_TRY(ctx->w_signer.ensure(nsigs * 4 + 4), "ws signer");
-    NW_TRY(ctx->w_cert_first.ensure(ncerts * 4 + 4), "ws first");
-    NW_TRY(ctx->w_cert_n.ensure(ncerts * 4 + 4), "ws n");
-    NW_TRY(ctx->w_msg.ensure(ncerts * 32 + 32), "ws msg");
-    NW_TRY(ctx->w_cert_ok.ensure(ncerts + 16), "ws cert_ok");
-    NW_TRY(ctx->w_stake_out.ensure(ncerts * 8 + 8), "ws stake");
-    NW_TRY(ctx->w_ok.ensure(nsigs + 16), "ws ok");
-    hipStream_t st = ctx->stream;
+    if (ncerts == 0) return NW_OK;   // nothing to verify (nsigs is 0 too)
+    // one staged H2D of every input and one D2H of every output (single-certificate latency)
+    const size_t o_sig = 0, o_signer = align256(o_sig + nsigs * 64), o_first = align256(o_signer + nsigs * 4),
+                 o_nv = align256(o_first + ncerts * 4), o_msg = align256(o_nv + ncerts * 4),
+                 in_bytes = align256(o_msg + ncerts * 32);
+    const size_t o_cok = 0, o_stake = align256(ncerts), o_ok = align256(o_stake + ncerts * 8),
+                 out_bytes = align256(o_ok + nsigs);
+    NW_TRY(ctx->w_io.ensure(in_bytes + out_bytes), "ws io");
+    NW_TRY(ctx->h_io.ensure(in_bytes > out_bytes ? in_bytes : out_bytes), "pinned io");
+    uint8_t* h = ctx->h_io.bytes();
     if (nsigs) {
-        NW_TRY(hipMemcpyAsync(ctx->w_sig.p, sig, nsigs * 64, hipMemcpyHostToDevice, st), "H2D sig");
-        NW_TRY(hipMemcpyAsync(ctx->w_signer.p, signer_slot, nsigs * 4, hipMemcpyHostToDevice, st), "H2D signer");
+        std::memcpy(h + o_sig, sig, nsigs * 64);
+        std::memcpy(h + o_signer, signer_slot, nsigs * 4);
     }
     if (ncerts) {
-        NW_TRY(hipMemcpyAsync(ctx->w_cert_first.p, first.data(), ncerts * 4, hipMemcpyHostToDevice, st), "H2D first");
-        NW_TRY(hipMemcpyAsync(ctx->w_cert_n.p, nv.data(), ncerts * 4, hipMemcpyHostToDevice, st), "H2D n");
-        NW_TRY(hipMemcpyAsync(ctx->w_msg.p, msg, ncerts * 32, hipMemcpyHostToDevice, st), "H2D msg");
+        std::memcpy(h + o_first, first.data(), ncerts * 4);
+        std::memcpy(h + o_nv, nv.data(), ncerts * 4);
+        std::memcpy(h + o_msg, msg, ncerts * 32);
     }
-    int rc = enqueue_certs(ctx, ncerts, ctx->w_cert_first.as<uint32_t>(), ctx->w_cert_n.as<uint32_t>(), nsigs,
-                           ctx->w_sig.as<uint8_t>(), ctx->w_signer.as<uint32_t>(), 0, ctx->w_msg.as<uint8_t>(), nullptr,
-                           nullptr, nullptr, zseed, cert_base, 1, ctx->w_cert_ok.as<uint8_t>(), nullptr,
-                           ctx->w_stake_out.as<uint64_t>(), st);
+    uint8_t* d_in = ctx->w_io.as<uint8_t>();
+    uint8_t* d_out = d_in + in_bytes;
+    hipStream_t st = ctx->stream;
+    NW_TRY(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, st), "H2D inputs");
+    int rc = enqueue_certs(ctx, ncerts, reinterpret_cast<const uint32_t*>(d_in + o_first),
+                           reinterpret_cast<const uint32_t*>(d_in + o_nv), nsigs, d_in + o_sig,
+                           reinterpret_cast<const uint32_t*>(d_in + o_signer), 0, d_in + o_msg, nullptr, nullptr,
+                           nullptr, zseed, cert_base, 1, d_out + o_cok, nullptr,
+                           reinterpret_cast<uint64_t*>(d_out + o_stake), st);
     if (rc != NW_OK) return rc;
-    if (sig_ok && nsigs) {
-        NW_TRY(launch_flags_to_ok((uint32_t)nsigs, ctx->w_flags.as<uint32_t>(), ctx->w_ok.as<uint8_t>(), st),
-               "k_flags_to_ok");
-        NW_TRY(hipMemcpyAsync(sig_ok, ctx->w_ok.p, nsigs, hipMemcpyDeviceToHost, st), "D2H sig_ok");
-    }
-    if (cert_ok && ncerts) NW_TRY(hipMemcpyAsync(cert_ok, ctx->w_cert_ok.p, ncerts, hipMemcpyDeviceToHost, st), "D2H");
-    if (accepted_stake && ncerts)
-        NW_TRY(hipMemcpyAsync(accepted_stake, ctx->w_stake_out.p, ncerts * 8, hipMemcpyDeviceToHost, st), "D2H");
+    if (sig_ok && nsigs)
+        NW_TRY(launch_flags_to_ok((uint32_t)nsigs, ctx->w_flags.as<uint32_t>(), d_out + o_ok, st), "k_flags_to_ok");
+    // the H2D above has completed in stream order before this copy overwrites the staging buffer
+    NW_TRY(hipMemcpyAsync(h, d_out, out_bytes, hipMemcpyDeviceToHost, st), "D2H outputs");
     NW_TRY(hipStreamSynchronize(st), "sync");
+    if (sig_ok && nsigs) std::memcpy(sig_ok, h + o_ok, nsigs);
+    if (cert_ok && ncerts) std::memcpy(cert_ok, h + o_cok, ncerts);
+    if (accepted_stake && ncerts) std::memcpy(accepted_stake, h + o_stake, ncerts * 8);
     return NW_OK;
 }
 
