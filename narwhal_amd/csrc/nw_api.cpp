@@ -285,10 +285,11 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
     if (batch_mode) NW_TRY(ctx->w_slow_buf.ensure(nsigs * (size_t)SLOW_WORDS * 4 + 4), "ws slow_buf");
     NW_TRY(ctx->w_pbuf.ensure(nsigs * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
     NW_TRY(ctx->w_pre.ensure(nsigs * 40 + 16), "ws pre");
-    NW_TRY(hipMemsetAsync(ctx->w_slow_count.p, 0, 16, st), "memset");
     // votes not covered by any certificate map to certificate 0 (never out of range)
     NW_TRY(hipMemsetAsync(ctx->w_sig_cert.p, 0, nsigs * 4 + 4, st), "memset sig_cert");
-    NW_TRY(launch_expand_certs((uint32_t)ncerts, d_first, d_nv, ctx->w_sig_cert.as<uint32_t>(), st), "k_expand_certs");
+    NW_TRY(launch_expand_certs((uint32_t)ncerts, d_first, d_nv, ctx->w_sig_cert.as<uint32_t>(),
+                               ctx->w_slow_count.as<uint32_t>(), st),
+           "k_expand_certs");   // also zeroes the slow-path counter
 
     VerifyParams vp{};
     vp.n = (uint32_t)nsigs;

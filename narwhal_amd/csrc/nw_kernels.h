@@ -68,8 +68,9 @@ hipError_t launch_group_by_signer(uint32_t n, uint32_t nkeys, const uint32_t* si
                                   uint32_t* cursor, uint32_t* perm, hipStream_t st);
 hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st);
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st);
+// Also zeroes zero4[0..3] (the slow-path counter) when ncerts > 0, saving a memset launch.
 hipError_t launch_expand_certs(uint32_t ncerts, const uint32_t* first, const uint32_t* nv, uint32_t* sig_cert,
-                               hipStream_t st);
+                               uint32_t* zero4, hipStream_t st);
 hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hipStream_t st);
 hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
                            uint32_t* tab, int window, hipStream_t st);

@@ -212,8 +212,9 @@ __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
 }
 
 __global__ void __launch_bounds__(256) k_expand_certs(uint32_t ncerts, const uint32_t* cert_first,
-                                                      const uint32_t* cert_n, uint32_t* sig_cert) {
+                                                      const uint32_t* cert_n, uint32_t* sig_cert, uint32_t* zero4) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < 4) zero4[c] = 0u;   // ncerts >= 1: the launch has at least 256 threads
     if (c >= ncerts) return;
     const uint32_t f = cert_first[c], n = cert_n[c];
     for (uint32_t v = 0; v < n; ++v) sig_cert[f + v] = c;
@@ -354,10 +355,10 @@ hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
 }
 
 hipError_t launch_expand_certs(uint32_t ncerts, const uint32_t* first, const uint32_t* nv, uint32_t* sig_cert,
-                               hipStream_t st) {
-    if (ncerts == 0) return hipSuccess;
+                               uint32_t* zero4, hipStream_t st) {
+    if (ncerts == 0) return hipMemsetAsync(zero4, 0, 16, st);
     hipLaunchKernelGGL(k_expand_certs, dim3(blocks_for(ncerts, 256)), dim3(256), 0, st, ncerts, first, nv,
-                       sig_cert);
+                       sig_cert, zero4);
     return hipGetLastError();
 }
 
