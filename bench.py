@@ -6,19 +6,32 @@ one full pass of the hot path over that batch: per-vote strict verdicts + per-ce
 verdicts + accepted stake (nw_verify_certs_dev), then (N > 1) an RCCL all-gather of the per-shard
 verdict bitmaps and stake tallies — the only collective the path has.
 
+``python bench.py --gpus N`` with N > 1 and no torch.distributed environment re-launches itself as
+N ranks (``torch.distributed.run``, one process per GPU, 127.0.0.1 rendezvous) from a parent that
+never touches the GPU; under the driver's own ``torch.distributed.run`` it runs as one rank.
+
 Prints ONE JSON line (rank 0):
   * ``roofline`` — the dominant kernel, k_verify, timed with HIP events that libnwcrypto records on
     the launch stream around each k_verify launch (nw_profile_*).  ``achieved`` = the kernel's
     algorithmic u32 multiply-accumulates per launch (work model below) / average launch time;
     ``peak`` = the measured v_mad_u64_u32 rate (tools/valu_peak.hip -> profiles/r01_valu_peak.json).
   * ``cpu_baseline`` — the oracle's C restatement of dalek 1.0.1 (oracle/nw_ref.c, "port") timed on
-    the host cores on a bounded sample of the same certificates.
-  * ``digest`` — the worker's bulk SHA-512 (worker/src/processor.rs:65) over the C4 batch shape
-    (bincode batches of 977 x 512-B transactions), GPU vs hashlib on one host core.
+    every host core this process may run on, on a bounded sample of the same certificates; the
+    per-GPU share of that host (cores / 8 GPUs) is reported beside it.
+  * ``host_fed`` — the same C2 certificates through nw_verify_certs from host buffers (PCIe
+    included), several calls in flight so copies overlap compute: what the Rust drop-in sees.
+  * ``digest`` — the worker's bulk SHA-512 (worker/src/processor.rs:65) over bincode batches of
+    977 x 512-B transactions: node load and the C4 per-GPU share, host->device copy included,
+    concurrently with a verify step on a second stream, the single-chain bound, and hashlib on
+    every host core.
+  * ``msm`` — the variable-base Pippenger path (keys outside the committee cache) at the worker's
+    load shape: 64 verify_batch chunks of ~977 signatures over fresh keys.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,6 +46,7 @@ COST_MODEL_V1_FM = {3: 1750, 67: 1030, 667: 811, 977: 775, 6667: 644}
 MADS_PER_FM = 100          # 10 x 10 radix-2^25.5 limb products per field multiplication
 B_WINDOW = 24              # default basepoint comb window (nw_point.h; the library reports its own)
 MADD_FM = 7                # mixed (affine Niels) addition = 7 field multiplications
+GPUS_PER_NODE = 8
 
 
 def comb_pos(w):
@@ -66,14 +80,31 @@ def traffic_per_launch():
         return json.load(f).get("hbm_bytes_per_launch")
 
 
+def host_cores():
+    """Host threads this process may run on (the whole host unless the scheduler restricts it)."""
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(cs, com, seconds):
-    """Oracle restatement timed on host cores (rank 0, N = 1 only): bounded sample of certificates."""
+    """Oracle restatement timed on the host cores (rank 0, N = 1 only): bounded sample of
+    certificates.  Default thread count = every core in this process's affinity mask."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import nw_ref   # C restatement of dalek's u64 backend (oracle/nw_ref.c); test/baseline only
-    threads = int(os.environ.get("NW_CPU_THREADS", "16"))
+    threads = int(os.environ.get("NW_CPU_THREADS", "0")) or host_cores()
     zseed = bytes(32)
     done_sigs = done_certs = 0
-    per_call = 64
+    per_call = max(64, 4 * threads)
     c = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
@@ -84,86 +115,209 @@ def cpu_baseline(cs, com, seconds):
         done_sigs += int(sum(int(cs.cert_n[x]) for x in sel))
         c += per_call
     dt = time.perf_counter() - t0
-    return {"value": done_sigs / dt, "unit": "sigs/s", "cores": threads, "kind": "port",
+    rate = done_sigs / dt
+    return {"value": rate, "unit": "sigs/s", "cores": threads, "kind": "port",
+            "per_gpu_share": {"value": rate / GPUS_PER_NODE, "cores": threads / GPUS_PER_NODE,
+                              "note": "host rate / %d GPUs per node" % GPUS_PER_NODE},
+            "cpu_model": cpu_model(),
             "sample": "%d certificates x %d votes of the C2 workload (%d sigs) in %.1f s on %d threads; "
                       "oracle/nw_ref.c (C restatement of ed25519-dalek 1.0.1 u64 backend: per-vote A "
                       "decompression + Straus MSM, as crypto/src/lib.rs:206-219)"
                       % (done_certs, int(cs.cert_n[0]), done_sigs, dt, threads)}
 
 
-def digest_leg(eng, dev, n_batches, reps, cpu_seconds):
-    """Worker batch digests: SHA-512 of n_batches bincode batches resident in HBM (one lane per
-    batch: each batch is one sequential compression chain), plus the saturated kernel rate on
-    many short messages and hashlib on one host core."""
-    import hashlib
+def host_fed(eng, cs, slots, zseed, chunks=8, threads=4):
+    """C2 through nw_verify_certs from host buffers: ``chunks`` calls over ``threads`` host threads,
+    so one call's host->device copy overlaps another's kernels (each call has its own stream)."""
+    from concurrent.futures import ThreadPoolExecutor
     import numpy as np
+    bounds = np.linspace(0, cs.ncerts, chunks + 1).astype(int)
+    parts = []
+    for a, b in zip(bounds, bounds[1:]):
+        f0, f1 = int(cs.cert_first[a]), int(cs.cert_first[b - 1] + cs.cert_n[b - 1])
+        parts.append((cs.cert_first[a:b] - f0, cs.cert_n[a:b], np.ascontiguousarray(cs.sigs[f0:f1]),
+                      np.ascontiguousarray(slots[cs.signer[f0:f1]]), np.ascontiguousarray(cs.msgs[a:b]), int(a)))
+
+    def run(p):
+        ok, _, _ = eng.verify_certs_np(p[0], p[1], p[2], p[3], p[4], zseed, p[5])
+        return bool(ok.all())
+
+    with ThreadPoolExecutor(threads) as ex:
+        assert all(ex.map(run, parts))   # warm every workspace
+        t0 = time.perf_counter()
+        ok = all(ex.map(run, parts))
+        dt = time.perf_counter() - t0
+    assert ok
+    return {"value": cs.nsigs / dt, "unit": "sigs/s", "ms": dt * 1e3,
+            "note": "nw_verify_certs on pageable host buffers (pinned staging + one H2D/D2H per call), "
+                    "%d calls on %d threads; PCIe included" % (chunks, threads)}
+
+
+def digest_leg(eng, dev, n_node, n_share, reps, cpu_seconds, verify_step):
+    """Worker batch digests (worker/src/processor.rs:65), one lane per batch (each batch is one
+    sequential SHA-512 compression chain)."""
+    import hashlib
     import torch
+    from concurrent.futures import ThreadPoolExecutor
     from narwhal_amd import workload
     out = {}
-    host = workload.worker_batches_np(n_batches)
+    host = workload.worker_batches_np(n_node)
     blen = host.shape[1]
-    d_data = torch.from_numpy(host.reshape(-1)).to(dev)
-    d_off = torch.arange(n_batches, dtype=torch.int64, device=dev) * blen
-    d_len = torch.full((n_batches,), blen, dtype=torch.int64, device=dev)
-    d_out = torch.empty((n_batches, 64), dtype=torch.uint8, device=dev)
+    blocks = (blen + 17 + 127) // 128
+    st = torch.cuda.current_stream()
 
-    def run(nb, d_data, d_off, d_len, d_out, reps):
-        st = torch.cuda.current_stream()
-        eng.sha512_many_dev(d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), nb, d_out.data_ptr(),
-                            st.cuda_stream)
+    def dev_bufs(nb):
+        d_off = torch.arange(nb, dtype=torch.int64, device=dev) * blen
+        d_len = torch.full((nb,), blen, dtype=torch.int64, device=dev)
+        d_out = torch.empty((nb, 64), dtype=torch.uint8, device=dev)
+        return d_off, d_len, d_out
+
+    def timed(fn, reps, stream):
+        fn()
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(st)
+        e0.record(stream)
         for _ in range(reps):
-            eng.sha512_many_dev(d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), nb, d_out.data_ptr(),
-                                st.cuda_stream)
-        e1.record(st)
+            fn()
+        e1.record(stream)
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps / 1e3
 
-    t = run(n_batches, d_data, d_off, d_len, d_out, reps)
-    padded = n_batches * ((blen + 17 + 127) // 128) * 128
+    def dig(nb, d_data, d_off, d_len, d_out, stream):
+        return lambda: eng.sha512_many_dev(d_data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), nb,
+                                           d_out.data_ptr(), stream.cuda_stream)
+
+    d_data = torch.from_numpy(host.reshape(-1)).to(dev)
+    d_off, d_len, d_out = dev_bufs(n_node)
+    t = timed(dig(n_node, d_data, d_off, d_len, d_out, st), reps, st)
     got = d_out[:4].cpu().numpy()
     for b in range(4):
         assert bytes(got[b]) == hashlib.sha512(host[b].tobytes()).digest(), "GPU batch digest mismatch"
-    out["workload"] = "%d worker batches x %d B (977 x 512-B tx, bincode WorkerMessage::Batch)" % (n_batches, blen)
-    out["GBps"] = n_batches * blen / t / 1e9
-    out["batches_per_s"] = n_batches / t
+    padded = n_node * blocks * 128
+    out["workload"] = "%d worker batches x %d B (977 x 512-B tx, bincode WorkerMessage::Batch)" % (n_node, blen)
+    out["GBps"] = n_node * blen / t / 1e9
     out["kernel_ms"] = t * 1e3
     out["roofline_hbm"] = {"achieved": padded / t / 1e9, "peak": 8000.0, "unit": "GB/s",
                            "frac": padded / t / 1e9 / 8000.0}
-    del d_data, d_off, d_len, d_out
+    # single-chain bound: one batch alone on the GPU
+    t1 = timed(dig(1, d_data, d_off[:1], d_len[:1], d_out, st), 2, st)
+    out["single_chain"] = {"blocks_per_batch": blocks, "lone_batch_ms": t1 * 1e3, "ns_per_block": t1 / blocks * 1e9,
+                           "bound_GBps": {str(n): n * blen / t1 / 1e9 for n in (n_share, n_node)},
+                           "note": "a batch is one sequential chain of %d compressions: wall time >= lone-batch "
+                                   "time whatever the batch count, until the lanes exceed the SIMDs" % blocks}
+    # C4 per-GPU share: 1,250 batches; alone, with the host->device copy from pinned memory, and
+    # concurrently with the C2 verify step on a second stream
+    pinned = torch.from_numpy(host[:n_share].reshape(-1)).pin_memory()
+    d_share = torch.empty(pinned.shape, dtype=torch.uint8, device=dev)
+    s_off, s_len, s_out = dev_bufs(n_share)
+    ts = timed(dig(n_share, d_share, s_off, s_len, s_out, st), reps, st)
+
+    def h2d_and_digest():
+        d_share.copy_(pinned, non_blocking=True)
+        dig(n_share, d_share, s_off, s_len, s_out, st)()
+
+    th = timed(h2d_and_digest, reps, st)
+    assert bytes(s_out[n_share - 1].cpu().numpy()) == hashlib.sha512(host[n_share - 1].tobytes()).digest()
+    s2 = torch.cuda.Stream(device=dev)
+    tv = timed(lambda: verify_step(st), reps, st)
+
+    def both():
+        with torch.cuda.stream(s2):
+            d_share.copy_(pinned, non_blocking=True)
+            dig(n_share, d_share, s_off, s_len, s_out, s2)()
+        verify_step(st)
+
+    torch.cuda.synchronize()
+    both()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        both()
+    torch.cuda.synchronize()
+    tb = (time.perf_counter() - t0) / reps
+    out["c4_share"] = {"batches": n_share, "kernel_ms": ts * 1e3, "GBps": n_share * blen / ts / 1e9,
+                       "with_h2d_ms": th * 1e3, "with_h2d_GBps": n_share * blen / th / 1e9,
+                       "verify_step_ms": tv * 1e3, "overlapped_ms": tb * 1e3,
+                       "overlap_saving_ms": (th + tv - tb) * 1e3,
+                       "note": "overlapped = H2D + digest of the share on a second stream concurrently with "
+                               "one C2 verify step (1,000,042 sigs) on the first"}
+    del d_data, d_off, d_len, d_out, d_share, pinned
     # saturated rate: 2^21 independent 1 KiB messages (enough concurrent chains to fill every SIMD)
     ns, ml = 1 << 21, 1024
     g = torch.Generator(device="cpu").manual_seed(7)
     small = torch.randint(0, 256, (ns * ml,), dtype=torch.uint8, generator=g)
     d_small = small.to(dev)
-    s_off = torch.arange(ns, dtype=torch.int64, device=dev) * ml
-    s_len = torch.full((ns,), ml, dtype=torch.int64, device=dev)
-    s_out = torch.empty((ns, 64), dtype=torch.uint8, device=dev)
-    ts = run(ns, d_small, s_off, s_len, s_out, reps)
-    chk = s_out[:2].cpu().numpy()
+    q_off = torch.arange(ns, dtype=torch.int64, device=dev) * ml
+    q_len = torch.full((ns,), ml, dtype=torch.int64, device=dev)
+    q_out = torch.empty((ns, 64), dtype=torch.uint8, device=dev)
+    tq = timed(dig(ns, d_small, q_off, q_len, q_out, st), reps, st)
+    chk = q_out[:2].cpu().numpy()
     sm = small[:2 * ml].numpy()
     for b in range(2):
         assert bytes(chk[b]) == hashlib.sha512(sm[b * ml:(b + 1) * ml].tobytes()).digest()
-    out["valu_ceiling_GBps"] = ns * ((ml + 17 + 127) // 128) * 128 / ts / 1e9
+    out["valu_ceiling_GBps"] = ns * ((ml + 17 + 127) // 128) * 128 / tq / 1e9
     out["roofline_valu"] = {"achieved": out["roofline_hbm"]["achieved"], "peak": out["valu_ceiling_GBps"],
                             "unit": "GB/s", "frac": out["roofline_hbm"]["achieved"] / out["valu_ceiling_GBps"],
                             "note": "peak = same kernel on 2^21 x 1 KiB messages (saturated SHA-512 VALU rate)"}
-    del d_small, s_off, s_len, s_out
+    del d_small, q_off, q_len, q_out
     if cpu_seconds > 0:
+        threads = host_cores()
+        stop = time.perf_counter() + cpu_seconds
+
+        def hash_loop(k):
+            nb = 0
+            while time.perf_counter() < stop:
+                hashlib.sha512(host[(k + nb) % n_node].data).digest()
+                nb += 1
+            return nb
+
         t0 = time.perf_counter()
-        nb = 0
-        while time.perf_counter() - t0 < cpu_seconds:
-            hashlib.sha512(host[nb % n_batches].tobytes()).digest()
-            nb += 1
+        with ThreadPoolExecutor(threads) as ex:
+            nb = sum(ex.map(hash_loop, range(threads)))
         dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"GBps": nb * blen / dt / 1e9, "cores": 1, "kind": "hashlib (OpenSSL) SHA-512",
-                               "sample": "%d batches in %.1f s" % (nb, dt)}
+        out["cpu_baseline"] = {"GBps": nb * blen / dt / 1e9, "cores": threads, "kind": "hashlib (OpenSSL) SHA-512",
+                               "per_gpu_share_GBps": nb * blen / dt / 1e9 / GPUS_PER_NODE,
+                               "sample": "%d batches in %.1f s on %d threads" % (nb, dt, threads)}
     return out
 
 
-def main():
+def msm_leg(eng, n_sigs=62500, chunks=64, reps=3):
+    """Keys outside the committee cache (the worker's direct verify_batch, worker/src/processor.rs:
+    75-79, without loading its keys): nw_verify_batches_pk -> Pippenger MSM, host buffers."""
+    import numpy as np
+    from narwhal_amd import workload
+    seeds = np.frombuffer(workload._chacha20_keystream(32 * n_sigs), np.uint8).reshape(n_sigs, 32)
+    seeds = seeds[::-1].copy()   # not the committee's keys
+    msgs = np.arange(n_sigs, dtype="<u8").view(np.uint8).reshape(n_sigs, 8).copy()
+    pks, sigs = eng.sign_many_np(seeds, msgs)
+    counts = [min(n_sigs, (n_sigs * (c + 1)) // chunks) - (n_sigs * c) // chunks for c in range(chunks)]
+    zseed = os.urandom(32)
+    ok = eng.verify_batches_pk_np(counts, msgs, pks, sigs, zseed, 0)
+    assert ok.all(), "MSM path rejected honest batches"
+    t0 = time.perf_counter()
+    for r in range(reps):
+        ok = eng.verify_batches_pk_np(counts, msgs, pks, sigs, zseed, chunks * (r + 1))
+    dt = (time.perf_counter() - t0) / reps
+    assert ok.all()
+    return {"value": n_sigs / dt, "unit": "sigs/s", "ms": dt * 1e3,
+            "workload": "%d verify_batch chunks, %d sigs, 8-byte messages, fresh (uncached) keys" % (chunks, n_sigs),
+            "note": "host-buffer path incl. PCIe and host packing; per-kernel times in profiles/r02/"}
+
+
+def launch_ranks(args, argv):
+    """--gpus N outside torch.distributed: one rank per GPU via torch.distributed.run, started from
+    this process before it touches the GPU; returns the launcher's exit status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def parse_args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -175,22 +329,66 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-samples", type=int, default=200)
     ap.add_argument("--digest-batches", type=int, default=10000, help="0 disables the digest leg")
+    ap.add_argument("--digest-share", type=int, default=1250, help="C4 per-GPU batch share")
+    ap.add_argument("--no-extras", action="store_true", help="headline only (no host_fed / msm legs)")
     ap.add_argument("--key-window", type=int, default=-1,
                     help="key comb window; -1 = committee mode (library sizes it for the loaded committee)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher check without a GPU: ranks meet over gloo, rank 0 prints the world")
+    return ap.parse_args(argv)
+
+
+def dry_run(args):
+    """Rank plumbing of ``--gpus N`` on CPU (tests/test_bench_launch.py): one gloo all_gather of
+    the rank ids, the same barrier/max-over-ranks pattern as the timed loop, one JSON line."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    ids = torch.tensor([rank], dtype=torch.int64)
+    got = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    if world > 1:
+        dist.all_gather(got, ids)
+        el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    else:
+        got = [ids]
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_arg": args.gpus,
+                          "ranks": [int(g.item()) for g in got],
+                          "local_ranks_env": os.environ.get("LOCAL_RANK")}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, argv)
+    if args.dry_run:
+        return dry_run(args)
 
     import numpy as np
     import torch
     import torch.distributed as dist
+    from narwhal_amd import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    from narwhal_amd import _lib, shard, workload
+    from narwhal_amd import _lib, workload
     eng = _lib.Engine(device=local, key_window=args.key_window)
     com = workload.make_committee(args.validators, eng)
     slots = eng.committee_load_np(com.pks, com.stake)
@@ -206,21 +404,24 @@ def main():
     d_ok = torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev)
     d_flags = torch.zeros(cs.nsigs, dtype=torch.int32, device=dev)
     d_stake = torch.zeros(cs.ncerts, dtype=torch.int64, device=dev)
+    d_status = torch.zeros(1, dtype=torch.int32, device=dev)   # asynchronous input check (NW_OK / NW_ERR_ARG)
     ranges = [(r * args.certs, (r + 1) * args.certs) for r in range(world)]   # node-wide certificate ranges
     zseed = os.urandom(32)
 
-    def step():
-        stream = torch.cuda.current_stream().cuda_stream
+    def verify_step(stream):
         eng.verify_certs_dev(cs.ncerts, d_first.data_ptr(), d_n.data_ptr(), cs.nsigs, d_sig.data_ptr(),
                              d_signer.data_ptr(), d_msg.data_ptr(), zseed, first_cert, d_ok.data_ptr(),
-                             d_flags.data_ptr(), d_stake.data_ptr(), stream)
+                             d_flags.data_ptr(), d_stake.data_ptr(), stream.cuda_stream, d_status=d_status.data_ptr())
+
+    def step():
+        verify_step(torch.cuda.current_stream())
         if world > 1:
             shard.allgather_verdicts(d_ok, d_stake, ranges)   # RCCL all_gather of bitmaps + stake
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ok_all = bool(d_ok.all().item()) and bool((d_stake == args.votes).all().item())
+    ok_all = bool(d_ok.all().item()) and bool((d_stake == args.votes).all().item()) and int(d_status.item()) == 0
     if world > 1:
         dist.barrier()
     eng.profile_read()             # discard warmup events
@@ -302,15 +503,19 @@ def main():
             out["cpu_baseline"] = cpu_baseline(cs, com, args.cpu_seconds)
         else:
             out["cpu_baseline"] = None
+        if world == 1 and not args.no_extras:
+            out["host_fed"] = host_fed(eng, cs, slots, zseed)
         if world == 1 and args.digest_batches > 0:
-            del d_sig, d_signer, d_flags
-            out["digest"] = digest_leg(eng, dev, args.digest_batches, 3,
-                                       0.0 if args.no_cpu_baseline else 3.0)
+            out["digest"] = digest_leg(eng, dev, args.digest_batches, args.digest_share, 3,
+                                       0.0 if args.no_cpu_baseline else 3.0, verify_step)
+        if world == 1 and not args.no_extras:
+            out["msm"] = msm_leg(eng)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

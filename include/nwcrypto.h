@@ -4,8 +4,20 @@
  * C ABI drop-in boundary for the reference ``crypto`` crate's hot path.
  * Every entry point names the reference interface it replaces.  All buffers are caller-owned;
  * calls are synchronous unless the name ends in ``_dev`` (those enqueue on a caller stream and
- * take device pointers).  A context is safe to share between threads (calls serialize on it).
- * There is no CPU fallback: with no usable GPU every call returns NW_ERR_DEVICE.
+ * take device pointers).  There is no CPU fallback: with no usable GPU every call returns
+ * NW_ERR_DEVICE.
+ *
+ * Threading (the worker calls verify_batch from 64 rayon threads, worker/src/processor.rs:75-79):
+ * a context is reentrant.  Each call leases its own stream and scratch from a pool (up to 64
+ * concurrent calls; more wait), so calls from different threads run concurrently on the GPU.  The
+ * key cache is read-shared by verify calls; nw_committee_load takes it exclusively and waits for
+ * in-flight calls first.  A ``_dev`` call's scratch stays reserved until its work completes on the
+ * caller's stream.  nw_last_error() reports the calling thread's last error.
+ *
+ * Batch coefficients: every batch entry point takes ``zseed``, which MUST be 32 fresh CSPRNG bytes
+ * per call in production (the reference draws z_i from thread_rng on every call).  With a fixed or
+ * public seed an attacker can build invalid signatures whose batch terms cancel.  NULL is rejected
+ * with NW_ERR_ARG.
  *
  * Verdict semantics are those of ed25519-dalek 1.0.1 (default features + "batch"):
  *   strict  = crypto::Signature::verify      (crypto/src/lib.rs:200-204) -> verify_strict
@@ -41,6 +53,10 @@ extern "C" {
 #define NW_F_SLOW 0x1000u     /* needed the exact batch equation (rare path) */
 #define NW_F_R_BAD 0x2000u    /* R failed to decode (found on the exact path) */
 
+/* Opaque extended-point encoding exchanged between shards of one split batch
+ * (nw_verify_batch_partial / nw_points_sum_is_identity): 160 bytes. */
+#define NW_POINT_BYTES 160
+
 typedef struct nw_ctx nw_ctx;
 
 typedef struct nw_opts {
@@ -65,7 +81,7 @@ typedef struct nw_cert {
 /* ---- context ------------------------------------------------------------------------------- */
 int nw_ctx_create(nw_ctx** out, const nw_opts* opts);
 void nw_ctx_destroy(nw_ctx* ctx);
-/* Human-readable description of the last error on this context (thread-unsafe diagnostics). */
+/* Human-readable description of the calling thread's last error. */
 const char* nw_last_error(const nw_ctx* ctx);
 
 /* ---- committee / key cache -------------------------------------------------------------------
@@ -84,6 +100,12 @@ int nw_key_window(const nw_ctx* ctx);
 int nw_base_window(void);
 
 /* ---- verification ----------------------------------------------------------------------------
+ * Keys: nw_verify_strict[_many] and nw_verify_batch accept ANY key, like the reference (which
+ * decompresses every key per call, crypto/src/lib.rs:202,216).  When every key of a call is in the
+ * key cache the call uses the cached comb tables; otherwise it runs the variable-base path (strict:
+ * per-signature decompression + windowed scalar multiplication; batch: a Pippenger multi-scalar
+ * multiplication) and leaves the cache unchanged.  Verdicts are identical on both paths.
+ *
  * crypto::Signature::verify (crypto/src/lib.rs:200-204): strict single verify of ``msg``. */
 int nw_verify_strict(nw_ctx* ctx, const uint8_t* msg, size_t len, const uint8_t pk[32],
                      const uint8_t sig[64]);
@@ -100,6 +122,27 @@ int nw_verify_strict_many(nw_ctx* ctx, const uint8_t* const* msg, const size_t* 
 int nw_verify_batch(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len,
                     const uint8_t (*pk)[32], const uint8_t (*sig)[64], size_t n,
                     const uint8_t zseed[32], uint64_t batch_index);
+
+/* Many dalek::verify_batch calls over arbitrary keys in one submission (the worker's direct call,
+ * worker/src/processor.rs:78, without a key cache): batch b is the next counts[b] signatures;
+ * batch_ok[b] = 1 iff its batch equation holds (coefficients: NW-Z v1 with batch index
+ * batch_base + b).  Always the variable-base Pippenger path. */
+int nw_verify_batches_pk(nw_ctx* ctx, size_t nb, const uint32_t* counts, const uint8_t* const* msg,
+                         const size_t* len, const uint8_t (*pk)[32], const uint8_t (*sig)[64],
+                         const uint8_t zseed[32], uint64_t batch_base, uint8_t* batch_ok);
+
+/* One shard of a batch split across GPUs: the shard's share of the batch
+ * equation, sum z_i R_i + sum (z_i h_i mod l) A_i - (sum z_i s_i mod l) B over its n signatures,
+ * with z_i drawn at coefficient index z_offset + i of batch ``batch_index``.  ``point`` receives the
+ * sum (NW_POINT_BYTES, opaque); *bad = 1 when a signature fails to parse or decode (the batch is
+ * then Err).  The batch verdict is Ok iff no shard is bad and nw_points_sum_is_identity of all
+ * shards' points is true. */
+int nw_verify_batch_partial(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len,
+                            const uint8_t (*pk)[32], const uint8_t (*sig)[64], size_t n,
+                            const uint8_t zseed[32], uint64_t batch_index, uint32_t z_offset,
+                            uint8_t point[NW_POINT_BYTES], int* bad);
+int nw_points_sum_is_identity(nw_ctx* ctx, const uint8_t (*points)[NW_POINT_BYTES], size_t k,
+                              int* is_identity);
 
 /* Certificate bulk path (Certificate::verify's batch step, primary/src/messages.rs:214, for many
  * certificates at once).  Signers are committee slots (nw_committee_load).  msg[c] is the 32-byte
@@ -124,13 +167,21 @@ int nw_verify_batches(nw_ctx* ctx, size_t nb, const uint32_t* first, const uint3
                       uint8_t* sig_ok);
 
 /* Device-resident variant for streaming use (inputs already in HBM).  All pointers are device
- * pointers; ``stream`` is a hipStream_t (NULL = default stream).  Enqueues work and returns;
- * ``sig_flags`` (uint32 per vote, NW_F_* bits) may be NULL. */
+ * pointers; ``stream`` is a hipStream_t (NULL = default stream).  ``sig_flags`` (uint32 per vote,
+ * NW_F_* bits) may be NULL.  The inputs are checked on the device (every vote range inside
+ * [0, nsigs), every signer slot inside the key cache); the kernels clamp them, so bad inputs never
+ * fault — their signatures and certificates are rejected.
+ *   d_status == NULL: the check is synchronous — the call waits for it on ``stream`` and returns
+ *                     NW_ERR_ARG (enqueueing nothing else) when it fails; otherwise it enqueues the
+ *                     verification and returns.
+ *   d_status != NULL: fully asynchronous — *d_status (device uint32) receives NW_OK or NW_ERR_ARG
+ *                     in stream order. */
 int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first,
                         const uint32_t* d_cert_nvotes, size_t nsigs, const uint8_t* d_sig64,
                         const uint32_t* d_signer_slot, const uint8_t* d_msg32,
                         const uint8_t zseed[32], uint64_t cert_base, uint8_t* d_cert_ok,
-                        uint32_t* d_sig_flags, uint64_t* d_accepted_stake, void* stream);
+                        uint32_t* d_sig_flags, uint64_t* d_accepted_stake, uint32_t* d_status,
+                        void* stream);
 
 /* ---- digests ---------------------------------------------------------------------------------
  * sha2 0.9 Sha512 via ed25519_dalek::Sha512 (primary/src/messages.rs:72-82,147-151,228-232;

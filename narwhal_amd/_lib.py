@@ -74,7 +74,10 @@ def _load() -> ctypes.CDLL:
         "nw_verify_strict_many": (I, [P, P, P, P, P, S, P]),
         "nw_verify_batch": (I, [P, P, P, P, P, S, P, U64]),
         "nw_verify_certs": (I, [P, P, S, P, P, P, P, U64, P, P, P]),
-        "nw_verify_certs_dev": (I, [P, S, P, P, S, P, P, P, P, U64, P, P, P, P]),
+        "nw_verify_certs_dev": (I, [P, S, P, P, S, P, P, P, P, U64, P, P, P, P, P]),
+        "nw_verify_batches_pk": (I, [P, S, P, P, P, P, P, P, U64, P]),
+        "nw_verify_batch_partial": (I, [P, P, P, P, P, S, P, U64, U32, P, ctypes.POINTER(I)]),
+        "nw_points_sum_is_identity": (I, [P, P, S, ctypes.POINTER(I)]),
         "nw_verify_batches": (I, [P, S, P, P, P, P, P, P, P, U64, P, P]),
         "nw_sha512": (I, [P, P, S, P]),
         "nw_sha512_many": (I, [P, P, P, P, S, P]),
@@ -108,8 +111,12 @@ def _buf(b: bytes):
     return ctypes.c_char_p(b) if b else None
 
 
+POINT_BYTES = 160   # NW_POINT_BYTES
+
+
 class Engine:
-    """One nw_ctx (one GPU).  Thread-safe: the C layer serializes calls on a context."""
+    """One nw_ctx (one GPU).  Thread-safe and reentrant: every call leases its own stream and
+    scratch in the C layer, so calls from several threads run concurrently."""
 
     def __init__(self, device: int = -1, max_keys: int = 0, key_window: int = 0):
         self._ctx = ctypes.c_void_p()
@@ -323,11 +330,67 @@ class Engine:
         return cert_ok[:nc], sig_ok[:len(slots)], stake[:nc]
 
     def verify_certs_dev(self, ncerts, d_first, d_n, nsigs, d_sig, d_signer, d_msg, zseed: bytes, cert_base,
-                         d_cert_ok, d_flags, d_stake, stream):
-        """Device-pointer path (ints = device addresses, e.g. torch ``data_ptr()``); enqueues only."""
+                         d_cert_ok, d_flags, d_stake, stream, d_status=None):
+        """Device-pointer path (ints = device addresses, e.g. torch ``data_ptr()``).  With
+        ``d_status`` None the device-side input check is synchronous and a bad input raises
+        DeviceError (NW_ERR_ARG); with a device uint32 address it is written in stream order and the
+        call only enqueues."""
         self.check(LIB.nw_verify_certs_dev(self._ctx, ncerts, d_first, d_n, nsigs, d_sig, d_signer, d_msg,
-                                           bytes(zseed), cert_base, d_cert_ok, d_flags, d_stake, stream),
+                                           bytes(zseed), cert_base, d_cert_ok, d_flags, d_stake, d_status, stream),
                    "nw_verify_certs_dev")
+
+    def verify_batches_pk(self, counts, msgs, pks, sigs, zseed: bytes, batch_base: int = 0):
+        """Batches over arbitrary keys (variable-base Pippenger path): batch b is the next
+        counts[b] signatures.  msgs: list of bytes; pks/sigs: lists (or one joined bytes blob).
+        Returns a list of bools."""
+        nb = len(counts)
+        n = sum(counts)
+        if nb == 0:
+            return []
+        mp = (ctypes.c_char_p * max(n, 1))(*[bytes(m) for m in msgs])
+        ln = (ctypes.c_size_t * max(n, 1))(*[len(m) for m in msgs])
+        cnt = (ctypes.c_uint32 * nb)(*counts)
+        pkb = pks if isinstance(pks, (bytes, bytearray)) else b"".join(map(bytes, pks))
+        sgb = sigs if isinstance(sigs, (bytes, bytearray)) else b"".join(map(bytes, sigs))
+        ok = (ctypes.c_uint8 * nb)()
+        self.check(LIB.nw_verify_batches_pk(self._ctx, nb, cnt, mp, ln, _buf(bytes(pkb)), _buf(bytes(sgb)),
+                                            bytes(zseed), batch_base, ok), "nw_verify_batches_pk")
+        return [bool(x) for x in ok]
+
+    def verify_batches_pk_np(self, counts, msgs, pks, sigs, zseed: bytes, batch_base: int = 0):
+        """numpy variant: msgs uint8[N, L] (fixed length), pks uint8[N, 32], sigs uint8[N, 64]."""
+        import numpy as np
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        pks = np.ascontiguousarray(pks, dtype=np.uint8)
+        sigs = np.ascontiguousarray(sigs, dtype=np.uint8)
+        counts = np.ascontiguousarray(counts, dtype=np.uint32)
+        n, ml = msgs.shape
+        ptrs = (msgs.ctypes.data + np.arange(n, dtype=np.uint64) * ml).astype(np.uint64)
+        lens = np.full(n, ml, dtype=np.uint64)
+        ok = np.zeros(max(len(counts), 1), np.uint8)
+        self.check(LIB.nw_verify_batches_pk(self._ctx, len(counts), counts.ctypes.data, ptrs.ctypes.data,
+                                            lens.ctypes.data, pks.ctypes.data, sigs.ctypes.data, bytes(zseed),
+                                            batch_base, ok.ctypes.data), "nw_verify_batches_pk")
+        return ok[:len(counts)]
+
+    def verify_batch_partial(self, msgs, pks, sigs, zseed: bytes, batch_index: int, z_offset: int):
+        """One shard's share of a split batch: returns (point bytes[160], bad)."""
+        n = len(sigs)
+        mp = (ctypes.c_char_p * max(n, 1))(*[bytes(m) for m in msgs])
+        ln = (ctypes.c_size_t * max(n, 1))(*[len(m) for m in msgs])
+        pt = ctypes.create_string_buffer(POINT_BYTES)
+        bad = ctypes.c_int(0)
+        self.check(LIB.nw_verify_batch_partial(self._ctx, mp, ln, _buf(b"".join(map(bytes, pks))),
+                                               _buf(b"".join(map(bytes, sigs))), n, bytes(zseed), batch_index,
+                                               z_offset, pt, ctypes.byref(bad)), "nw_verify_batch_partial")
+        return pt.raw, bool(bad.value)
+
+    def points_sum_is_identity(self, points) -> bool:
+        blob = b"".join(bytes(p) for p in points)
+        r = ctypes.c_int(0)
+        self.check(LIB.nw_points_sum_is_identity(self._ctx, _buf(blob), len(points), ctypes.byref(r)),
+                   "nw_points_sum_is_identity")
+        return bool(r.value)
 
     def profile_enable(self, on: bool = True):
         self.check(LIB.nw_profile_enable(self._ctx, 1 if on else 0), "nw_profile_enable")

@@ -1,20 +1,39 @@
-// C-ABI host layer of libnwcrypto (include/nwcrypto.h): device memory, the key cache, workspace,
-// and the launch sequences.  No CPU compute path: every verdict and digest comes from the GPU.
+// C-ABI host layer of libnwcrypto (include/nwcrypto.h): device memory, the key cache, per-call
+// workspaces and streams, and the launch sequences.  No CPU compute path: every verdict and digest
+// comes from the GPU.
+//
+// Concurrency model (the worker calls from 64 rayon threads,
+// worker/src/processor.rs:75-79):
+//   * the key cache (committee tables, basepoint comb) is shared state behind a reader/writer lock:
+//     every verify call holds it shared while it enqueues; nw_committee_load holds it exclusive and
+//     first waits for every in-flight call that may still read the tables;
+//   * every call leases a Workspace from a pool: its own stream, scratch buffers, pinned staging
+//     buffer and a completion event.  Host-buffer calls run on the workspace's stream and
+//     synchronize it; ``_dev`` calls run on the caller's stream and leave the workspace "pending"
+//     until its event completes — the next lease of that workspace waits on the event (stream
+//     order, or a host wait before any buffer is reallocated), so scratch is never reused while a
+//     kernel may still read it.
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <unordered_map>
 #include <vector>
 
 #include "nw_kernels.h"
+#include "nw_msm.h"
 #include "nw_point.h"
 
 using namespace nw;
 
 namespace {
+
+thread_local std::string tl_last_error;
 
 struct DevBuf {
     void* p = nullptr;
@@ -71,17 +90,49 @@ struct HostBuf {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Per-call scratch: one per concurrently executing call.
+struct Workspace {
+    hipStream_t stream = nullptr;   // stream of host-buffer calls
+    hipEvent_t done = nullptr;      // recorded after the last enqueue that used these buffers
+    hipStream_t last = nullptr;     // stream that event was recorded on
+    bool pending = false;
+    DevBuf w_sig, w_signer, w_keys, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len, w_flags,
+        w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_ok, w_misc, w_out, w_pbuf, w_pre, w_counts,
+        w_cursor, w_perm, w_io, w_var, w_status, w_msm_ent, w_msm_dig, w_msm_zs, w_msm_meta, w_msm_bkt, w_msm_part,
+        w_msm_wpart;
+    HostBuf h_io;
+
+    // Grow a buffer; a buffer that may still be read by a pending call is only freed after it.
+    hipError_t ensure(DevBuf& b, size_t bytes) {
+        if (bytes > b.cap && pending) {
+            hipError_t e = hipEventSynchronize(done);
+            if (e != hipSuccess) return e;
+            pending = false;
+        }
+        return b.ensure(bytes);
+    }
+    void release_all() {
+        for (DevBuf* b : {&w_sig, &w_signer, &w_keys, &w_sig_cert, &w_cert_first, &w_cert_n, &w_msg, &w_msg_off,
+                          &w_msg_len, &w_flags, &w_slow_count, &w_slow_list, &w_slow_slot, &w_slow_buf, &w_cert_ok,
+                          &w_ok, &w_misc, &w_out, &w_pbuf, &w_pre, &w_counts, &w_cursor, &w_perm, &w_io, &w_var,
+                          &w_status, &w_msm_ent, &w_msm_dig, &w_msm_zs, &w_msm_meta, &w_msm_bkt, &w_msm_part,
+                          &w_msm_wpart})
+            b->release();
+        h_io.release();
+    }
+};
+
+constexpr size_t kMaxWorkspaces = 64;   // one per concurrently calling thread (the worker's 64)
+
 }  // namespace
 
 struct nw_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;   // administrative stream: basepoint table, committee loads
     uint32_t finish_k = FINISH_K;   // k_finish signatures per lane
-    std::mutex mu;
-    std::string last_error;
-    // basepoint comb
+    // key cache (shared by all calls; guarded by keys_mu)
+    std::shared_mutex keys_mu;
     uint32_t* d_btab = nullptr;
-    // key cache
     size_t max_keys = 0;          // 0: derived from the HBM budget once the window is fixed
     bool max_keys_user = false;
     int key_window = 0;           // 0: not yet decided (first load)
@@ -93,24 +144,27 @@ struct nw_ctx {
     uint32_t* d_key_tab = nullptr;
     std::unordered_map<std::string, uint32_t> slot_of;
     std::vector<uint32_t> h_stake;
+    DevBuf w_bases;               // committee-load scratch (exclusive lock)
+    // workspace pool
+    std::mutex pool_mu;
+    std::condition_variable pool_cv;
+    std::vector<std::unique_ptr<Workspace>> pool;
+    std::vector<Workspace*> free_ws;
     // measurement: (start, stop) event pairs around k_verify launches
+    std::mutex prof_mu;
     bool prof_on = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> prof_events;
     size_t prof_used = 0;
     uint64_t prof_sigs = 0;
-    // workspace
-    DevBuf w_bases, w_sig, w_signer, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len,
-        w_flags, w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_stake_out, w_ok, w_misc,
-        w_out, w_pbuf, w_pre, w_counts, w_cursor, w_perm, w_io;
-    HostBuf h_io;
 };
 
 namespace {
 
+// Diagnostics are per calling thread (a context is shared by many threads).
+void set_error(nw_ctx*, const std::string& msg) { tl_last_error = msg; }
+
 int fail(nw_ctx* c, hipError_t e, const char* what) {
-    if (c) {
-        c->last_error = std::string(what) + ": " + hipGetErrorString(e);
-    }
+    set_error(c, std::string(what) + ": " + hipGetErrorString(e));
     return e == hipErrorOutOfMemory ? NW_ERR_NOMEM : NW_ERR_DEVICE;
 }
 
@@ -119,6 +173,81 @@ int fail(nw_ctx* c, hipError_t e, const char* what) {
         hipError_t e_ = (expr);                         \
         if (e_ != hipSuccess) return fail(ctx, e_, what); \
     } while (0)
+
+// Lease of a workspace for one call.  ``bind(st)`` orders the call after the workspace's previous
+// user; ``finish(st)`` records the completion event (kept pending for asynchronous calls).  A
+// host-buffer call that fails after enqueueing synchronizes its stream on release, so no DMA from
+// its pinned buffer and no kernel on its scratch outlives the call.
+class Lease {
+public:
+    explicit Lease(nw_ctx* ctx) : ctx_(ctx) {
+        std::unique_lock<std::mutex> g(ctx->pool_mu);
+        for (;;) {
+            if (!ctx->free_ws.empty()) {
+                ws_ = ctx->free_ws.back();
+                ctx->free_ws.pop_back();
+                return;
+            }
+            if (ctx->pool.size() < kMaxWorkspaces) break;
+            ctx->pool_cv.wait(g);
+        }
+        auto w = std::make_unique<Workspace>();
+        if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) return;
+        if (hipEventCreateWithFlags(&w->done, hipEventDisableTiming) != hipSuccess) {
+            (void)hipStreamDestroy(w->stream);
+            return;
+        }
+        ws_ = w.get();
+        ctx->pool.push_back(std::move(w));
+    }
+    ~Lease() {
+        if (!ws_) return;
+        if (sync_on_release_ && stream_) {
+            (void)hipStreamSynchronize(stream_);
+            ws_->pending = false;
+        }
+        std::lock_guard<std::mutex> g(ctx_->pool_mu);
+        ctx_->free_ws.push_back(ws_);
+        ctx_->pool_cv.notify_one();
+    }
+    Workspace* ws() const { return ws_; }
+    hipError_t bind(hipStream_t st, bool sync_on_release) {
+        stream_ = st;
+        sync_on_release_ = sync_on_release;
+        if (ws_->pending && ws_->last != st) return hipStreamWaitEvent(st, ws_->done, 0);
+        return hipSuccess;
+    }
+    hipError_t finish() {
+        hipError_t e = hipEventRecord(ws_->done, stream_);
+        if (e == hipSuccess) {
+            ws_->pending = true;
+            ws_->last = stream_;
+        }
+        return e;
+    }
+    // a host-buffer call that completed: its stream is idle
+    void synced() {
+        ws_->pending = false;
+        sync_on_release_ = false;
+    }
+
+private:
+    nw_ctx* ctx_;
+    Workspace* ws_ = nullptr;
+    hipStream_t stream_ = nullptr;
+    bool sync_on_release_ = false;
+};
+
+// Wait for every call that may still read the key tables (exclusive key lock held).
+int drain_all(nw_ctx* ctx) {
+    std::lock_guard<std::mutex> g(ctx->pool_mu);
+    for (auto& w : ctx->pool)
+        if (w->pending) {
+            NW_TRY(hipEventSynchronize(w->done), "drain");
+            w->pending = false;
+        }
+    return NW_OK;
+}
 
 // Basepoint encoding (y = 4/5, x even).
 const uint8_t kBaseEnc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
@@ -160,30 +289,39 @@ void fix_window(nw_ctx* ctx, size_t first_load) {
 int grow_keys(nw_ctx* ctx, size_t need) {
     if (need <= ctx->key_cap) return NW_OK;
     if (need > ctx->max_keys) {
-        ctx->last_error = "key cache capacity exceeded (nw_opts.max_keys)";
+        set_error(ctx, "key cache capacity exceeded (nw_opts.max_keys)");
         return NW_ERR_NOMEM;
     }
     size_t cap = ctx->key_cap ? ctx->key_cap : 64;
     while (cap < need) cap *= 2;
     if (cap > ctx->max_keys) cap = ctx->max_keys;
     uint32_t *raw = nullptr, *info = nullptr, *stake = nullptr, *tab = nullptr;
-    NW_TRY(hipMalloc(&raw, cap * 32), "hipMalloc(keys_raw)");
-    NW_TRY(hipMalloc(&info, cap * 4), "hipMalloc(key_info)");
-    NW_TRY(hipMalloc(&stake, cap * 4), "hipMalloc(stake)");
-    NW_TRY(hipMalloc(&tab, cap * ctx->key_words * 4), "hipMalloc(key_tab)");
-    if (ctx->nkeys) {
-        NW_TRY(hipMemcpyAsync(raw, ctx->d_keys_raw, ctx->nkeys * 32, hipMemcpyDeviceToDevice, ctx->stream), "copy");
-        NW_TRY(hipMemcpyAsync(info, ctx->d_key_info, ctx->nkeys * 4, hipMemcpyDeviceToDevice, ctx->stream), "copy");
-        NW_TRY(hipMemcpyAsync(stake, ctx->d_stake, ctx->nkeys * 4, hipMemcpyDeviceToDevice, ctx->stream), "copy");
-        NW_TRY(hipMemcpyAsync(tab, ctx->d_key_tab, ctx->nkeys * ctx->key_words * 4, hipMemcpyDeviceToDevice,
-                              ctx->stream),
-               "copy");
-        NW_TRY(hipStreamSynchronize(ctx->stream), "sync");
-        (void)hipFree(ctx->d_keys_raw);
-        (void)hipFree(ctx->d_key_info);
-        (void)hipFree(ctx->d_stake);
-        (void)hipFree(ctx->d_key_tab);
+    auto cleanup = [&]() {
+        for (uint32_t* p : {raw, info, stake, tab})
+            if (p) (void)hipFree(p);
+    };
+    hipError_t e = hipMalloc(&raw, cap * 32);
+    if (e == hipSuccess) e = hipMalloc(&info, cap * 4);
+    if (e == hipSuccess) e = hipMalloc(&stake, cap * 4);
+    if (e == hipSuccess) e = hipMalloc(&tab, cap * ctx->key_words * 4);
+    if (e == hipSuccess && ctx->nkeys) {
+        e = hipMemcpyAsync(raw, ctx->d_keys_raw, ctx->nkeys * 32, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(info, ctx->d_key_info, ctx->nkeys * 4, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(stake, ctx->d_stake, ctx->nkeys * 4, hipMemcpyDeviceToDevice, ctx->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(tab, ctx->d_key_tab, ctx->nkeys * ctx->key_words * 4, hipMemcpyDeviceToDevice,
+                               ctx->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     }
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(ctx->stream);
+        cleanup();
+        return fail(ctx, e, "grow key cache");
+    }
+    for (uint32_t* p : {ctx->d_keys_raw, ctx->d_key_info, ctx->d_stake, ctx->d_key_tab})
+        if (p) (void)hipFree(p);
     ctx->d_keys_raw = raw;
     ctx->d_key_info = info;
     ctx->d_stake = stake;
@@ -192,13 +330,14 @@ int grow_keys(nw_ctx* ctx, size_t need) {
     return NW_OK;
 }
 
-// Build tables for keys [k0, k0 + nk) whose raw bytes are already in d_keys_raw.
+// Build tables for nk keys whose raw bytes are already at d_raw (administrative stream).
 int build_keys(nw_ctx* ctx, uint32_t* d_raw, uint32_t* d_info, uint32_t* d_tab, size_t nk, int window) {
     // keys per launch: bounds the bases scratch and keeps a launch near 16M chunk threads
     const size_t chunk = window >= 24 ? 1 : (window == 20 ? 16 : (window == 16 ? 256 : 4096));
     const size_t words = comb_words(window);
     for (size_t s = 0; s < nk; s += chunk) {
         const size_t m = nk - s < chunk ? nk - s : chunk;
+        if (m * comb_pos(window) * 40 * 4 > ctx->w_bases.cap) NW_TRY(hipStreamSynchronize(ctx->stream), "sync");
         NW_TRY(ctx->w_bases.ensure(m * comb_pos(window) * 40 * 4), "hipMalloc(bases)");
         NW_TRY(launch_key_prep((uint32_t)m, d_raw + s * 8, d_info + s, ctx->w_bases.as<uint32_t>(), d_tab + s * words,
                                window, ctx->stream),
@@ -207,88 +346,95 @@ int build_keys(nw_ctx* ctx, uint32_t* d_raw, uint32_t* d_info, uint32_t* d_tab, 
     return NW_OK;
 }
 
-// Map keys to cache slots, loading unknown keys (table build on the GPU).
+// Slots of keys already in the cache (shared lock held).  Returns true when every key is cached.
+bool lookup_slots(nw_ctx* ctx, const uint8_t (*pk)[32], size_t n, uint32_t* slots) {
+    for (size_t i = 0; i < n; ++i) {
+        auto it = ctx->slot_of.find(std::string(reinterpret_cast<const char*>(pk[i]), 32));
+        if (it == ctx->slot_of.end()) return false;
+        slots[i] = it->second;
+    }
+    return true;
+}
+
+// Map keys to cache slots, loading unknown keys (table build on the GPU).  Exclusive lock held.
 int ensure_slots(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, size_t n, uint32_t* slots) {
-    std::vector<uint32_t> new_idx;
     std::vector<uint8_t> new_raw;
+    std::vector<uint32_t> new_stake;
+    std::vector<std::pair<uint32_t, uint32_t>> refresh;   // (slot, stake) of keys already cached
     std::unordered_map<std::string, uint32_t> pending;
     for (size_t i = 0; i < n; ++i) {
         std::string k(reinterpret_cast<const char*>(pk[i]), 32);
         auto it = ctx->slot_of.find(k);
         if (it != ctx->slot_of.end()) {
             slots[i] = it->second;
-            if (stake) {
-                ctx->h_stake[it->second] = stake[i];
-                new_idx.push_back(it->second);   // stake refresh only
-            }
+            if (stake) refresh.emplace_back(it->second, stake[i]);
             continue;
         }
         auto pit = pending.find(k);
         if (pit != pending.end()) {
             slots[i] = pit->second;
+            if (stake) new_stake[pit->second - ctx->nkeys] = stake[i];
             continue;
         }
         const uint32_t slot = (uint32_t)(ctx->nkeys + pending.size());
         pending.emplace(k, slot);
         slots[i] = slot;
         new_raw.insert(new_raw.end(), pk[i], pk[i] + 32);
-        ctx->h_stake.push_back(stake ? stake[i] : 0u);
+        new_stake.push_back(stake ? stake[i] : 0u);
     }
     const size_t add = pending.size();
+    if (add == 0 && refresh.empty()) return NW_OK;
+    int rc = drain_all(ctx);   // nothing in flight may read the tables or the stakes we change
+    if (rc != NW_OK) return rc;
     if (add && ctx->key_window <= 0) fix_window(ctx, add);
     if (add) {
-        int rc = grow_keys(ctx, ctx->nkeys + add);
-        if (rc != NW_OK) {
-            ctx->h_stake.resize(ctx->nkeys);
-            return rc;
-        }
+        rc = grow_keys(ctx, ctx->nkeys + add);
+        if (rc != NW_OK) return rc;
         const size_t k0 = ctx->nkeys;
         NW_TRY(hipMemcpyAsync(ctx->d_keys_raw + k0 * 8, new_raw.data(), add * 32, hipMemcpyHostToDevice, ctx->stream),
                "H2D keys");
         rc = build_keys(ctx, ctx->d_keys_raw + k0 * 8, ctx->d_key_info + k0, ctx->d_key_tab + k0 * ctx->key_words,
                         add, ctx->key_window);
-        if (rc != NW_OK) return rc;
-        for (auto& kv : pending) ctx->slot_of.emplace(kv.first, kv.second);
-        ctx->nkeys += add;
+        if (rc != NW_OK) {
+            (void)hipStreamSynchronize(ctx->stream);
+            return rc;
+        }
+        NW_TRY(hipStreamSynchronize(ctx->stream), "sync(key tables)");
     }
-    if (add || !new_idx.empty()) {
-        NW_TRY(hipMemcpyAsync(ctx->d_stake, ctx->h_stake.data(), ctx->nkeys * 4, hipMemcpyHostToDevice, ctx->stream),
-               "H2D stake");
-        NW_TRY(hipStreamSynchronize(ctx->stream), "sync(committee)");
-    }
+    // the host stake table changes only once the tables are built
+    std::vector<uint32_t> hs = ctx->h_stake;
+    hs.insert(hs.end(), new_stake.begin(), new_stake.end());
+    for (auto& r : refresh) hs[r.first] = r.second;
+    NW_TRY(hipMemcpyAsync(ctx->d_stake, hs.data(), hs.size() * 4, hipMemcpyHostToDevice, ctx->stream), "H2D stake");
+    NW_TRY(hipStreamSynchronize(ctx->stream), "sync(committee)");
+    for (auto& kv : pending) ctx->slot_of.emplace(kv.first, kv.second);
+    ctx->nkeys += add;
+    ctx->h_stake.swap(hs);
     return NW_OK;
 }
 
-void fill_zseed(uint32_t out[8], const uint8_t* zseed) {
-    if (!zseed) {
-        for (int k = 0; k < 8; ++k) out[k] = 0;
-        return;
-    }
-    std::memcpy(out, zseed, 32);
-}
-
-// Enqueue the certificate pipeline on device buffers.
-int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uint32_t* d_nv, size_t nsigs,
-                  const uint8_t* d_sig, const uint32_t* d_signer, int msgmode, const uint8_t* d_msg32,
+// Enqueue the certificate pipeline on device buffers (shared key lock held, workspace bound to st).
+int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_first, const uint32_t* d_nv,
+                  size_t nsigs, const uint8_t* d_sig, const uint32_t* d_signer, int msgmode, const uint8_t* d_msg32,
                   const uint8_t* d_msg_base, const uint64_t* d_msg_off, const uint64_t* d_msg_len,
                   const uint8_t* zseed, uint64_t cert_base, uint32_t batch_mode, uint8_t* d_cert_ok,
                   uint32_t* d_flags_user, uint64_t* d_stake_out, hipStream_t st) {
     uint32_t* d_flags = d_flags_user;
     if (!d_flags) {
-        NW_TRY(ctx->w_flags.ensure(nsigs * 4 + 4), "ws flags");
-        d_flags = ctx->w_flags.as<uint32_t>();
+        NW_TRY(ws->ensure(ws->w_flags, nsigs * 4 + 4), "ws flags");
+        d_flags = ws->w_flags.as<uint32_t>();
     }
-    NW_TRY(ctx->w_sig_cert.ensure(nsigs * 4 + 4), "ws sig_cert");
-    NW_TRY(ctx->w_slow_count.ensure(16), "ws slow_count");
-    NW_TRY(ctx->w_slow_list.ensure(nsigs * 4 + 4), "ws slow_list");
-    NW_TRY(ctx->w_slow_slot.ensure(nsigs * 4 + 4), "ws slow_slot");
-    if (batch_mode) NW_TRY(ctx->w_slow_buf.ensure(nsigs * (size_t)SLOW_WORDS * 4 + 4), "ws slow_buf");
-    NW_TRY(ctx->w_pbuf.ensure(nsigs * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
-    NW_TRY(ctx->w_pre.ensure(nsigs * 40 + 16), "ws pre");
+    NW_TRY(ws->ensure(ws->w_sig_cert, nsigs * 4 + 4), "ws sig_cert");
+    NW_TRY(ws->ensure(ws->w_slow_count, 16), "ws slow_count");
+    NW_TRY(ws->ensure(ws->w_slow_list, nsigs * 4 + 4), "ws slow_list");
+    NW_TRY(ws->ensure(ws->w_slow_slot, nsigs * 4 + 4), "ws slow_slot");
+    if (batch_mode) NW_TRY(ws->ensure(ws->w_slow_buf, nsigs * (size_t)SLOW_WORDS * 4 + 4), "ws slow_buf");
+    NW_TRY(ws->ensure(ws->w_pbuf, nsigs * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
+    NW_TRY(ws->ensure(ws->w_pre, nsigs * 40 + 16), "ws pre");
     // votes not covered by any certificate map to certificate 0 (never out of range)
-    NW_TRY(hipMemsetAsync(ctx->w_sig_cert.p, 0, nsigs * 4 + 4, st), "memset sig_cert");
-    NW_TRY(launch_expand_certs((uint32_t)ncerts, d_first, d_nv, ctx->w_sig_cert.as<uint32_t>(),
-                               ctx->w_slow_count.as<uint32_t>(), st),
+    NW_TRY(hipMemsetAsync(ws->w_sig_cert.p, 0, nsigs * 4 + 4, st), "memset sig_cert");
+    NW_TRY(launch_expand_certs((uint32_t)ncerts, (uint32_t)nsigs, d_first, d_nv, ws->w_sig_cert.as<uint32_t>(),
+                               ws->w_slow_count.as<uint32_t>(), st),
            "k_expand_certs");   // also zeroes the slow-path counter
 
     VerifyParams vp{};
@@ -296,7 +442,7 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
     vp.batch_mode = batch_mode;
     vp.sig = d_sig;
     vp.signer = d_signer;
-    vp.sig_cert = ctx->w_sig_cert.as<uint32_t>();
+    vp.sig_cert = ws->w_sig_cert.as<uint32_t>();
     vp.cert_first = d_first;
     vp.cert_msg = d_msg32;
     vp.msg_base = d_msg_base;
@@ -306,40 +452,45 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
     vp.keys_raw = ctx->d_keys_raw;
     vp.key_info = ctx->d_key_info;
     vp.key_tab = ctx->d_key_tab;
+    vp.nkeys = (uint32_t)ctx->nkeys;
     vp.btab = ctx->d_btab;
-    fill_zseed(vp.zseed, zseed);
+    static const uint8_t kNoSeed[32] = {0};   // strict-only calls draw no coefficients
+    std::memcpy(vp.zseed, zseed ? zseed : kNoSeed, 32);
     vp.flags = d_flags;
-    vp.slow_count = ctx->w_slow_count.as<uint32_t>();
-    vp.slow_list = ctx->w_slow_list.as<uint32_t>();
-    vp.slow_slot = ctx->w_slow_slot.as<uint32_t>();
-    vp.slow_buf = ctx->w_slow_buf.as<uint32_t>();
-    vp.pbuf = ctx->w_pbuf.as<uint32_t>();
-    vp.pre = ctx->w_pre.as<uint32_t>();
+    vp.slow_count = ws->w_slow_count.as<uint32_t>();
+    vp.slow_list = ws->w_slow_list.as<uint32_t>();
+    vp.slow_slot = ws->w_slow_slot.as<uint32_t>();
+    vp.slow_buf = ws->w_slow_buf.as<uint32_t>();
+    vp.pbuf = ws->w_pbuf.as<uint32_t>();
+    vp.pre = ws->w_pre.as<uint32_t>();
     vp.perm = nullptr;
     if (nsigs >= kGroupMinSigs && ctx->nkeys > 1) {
-        NW_TRY(ctx->w_counts.ensure(ctx->nkeys * 4 + 16), "ws counts");
-        NW_TRY(ctx->w_cursor.ensure(ctx->nkeys * 4 + 16), "ws cursor");
-        NW_TRY(ctx->w_perm.ensure(nsigs * 4 + 16), "ws perm");
-        NW_TRY(launch_group_by_signer((uint32_t)nsigs, (uint32_t)ctx->nkeys, d_signer, ctx->w_counts.as<uint32_t>(),
-                                      ctx->w_cursor.as<uint32_t>(), ctx->w_perm.as<uint32_t>(), st),
+        NW_TRY(ws->ensure(ws->w_counts, ctx->nkeys * 4 + 16), "ws counts");
+        NW_TRY(ws->ensure(ws->w_cursor, ctx->nkeys * 4 + 16), "ws cursor");
+        NW_TRY(ws->ensure(ws->w_perm, nsigs * 4 + 16), "ws perm");
+        NW_TRY(launch_group_by_signer((uint32_t)nsigs, (uint32_t)ctx->nkeys, d_signer, ws->w_counts.as<uint32_t>(),
+                                      ws->w_cursor.as<uint32_t>(), ws->w_perm.as<uint32_t>(), st),
                "signer grouping");
-        vp.perm = ctx->w_perm.as<uint32_t>();
+        vp.perm = ws->w_perm.as<uint32_t>();
     }
     vp.g0 = 0;
     vp.gn = (uint32_t)nsigs;
     vp.fk = ctx->finish_k;
     hipEvent_t ev_stop = nullptr;
-    if (ctx->prof_on && nsigs) {
-        if (ctx->prof_used == ctx->prof_events.size()) {
-            hipEvent_t a, b;
-            NW_TRY(hipEventCreate(&a), "hipEventCreate");
-            NW_TRY(hipEventCreate(&b), "hipEventCreate");
-            ctx->prof_events.emplace_back(a, b);
+    {
+        std::lock_guard<std::mutex> g(ctx->prof_mu);
+        if (ctx->prof_on && nsigs) {
+            if (ctx->prof_used == ctx->prof_events.size()) {
+                hipEvent_t a, b;
+                NW_TRY(hipEventCreate(&a), "hipEventCreate");
+                NW_TRY(hipEventCreate(&b), "hipEventCreate");
+                ctx->prof_events.emplace_back(a, b);
+            }
+            NW_TRY(hipEventRecord(ctx->prof_events[ctx->prof_used].first, st), "hipEventRecord");
+            ev_stop = ctx->prof_events[ctx->prof_used].second;
+            ++ctx->prof_used;
+            ctx->prof_sigs += nsigs;
         }
-        NW_TRY(hipEventRecord(ctx->prof_events[ctx->prof_used].first, st), "hipEventRecord");
-        ev_stop = ctx->prof_events[ctx->prof_used].second;
-        ++ctx->prof_used;
-        ctx->prof_sigs += nsigs;
     }
     NW_TRY(launch_verify(vp, msgmode, ctx->key_window, st), "k_verify");
     if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");   // brackets k_verify alone
@@ -350,6 +501,7 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
 
     FinalizeParams fp{};
     fp.ncerts = (uint32_t)ncerts;
+    fp.nsigs = (uint32_t)nsigs;
     fp.cert_first = d_first;
     fp.cert_n = d_nv;
     fp.flags = d_flags;
@@ -363,8 +515,9 @@ int enqueue_certs(nw_ctx* ctx, size_t ncerts, const uint32_t* d_first, const uin
     return NW_OK;
 }
 
-// Pack per-signature messages into one device buffer (MSGMODE 1).
-int upload_messages(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, size_t n) {
+// Pack per-signature messages into the workspace (MSGMODE 1).
+int upload_messages(nw_ctx* ctx, Workspace* ws, const uint8_t* const* msg, const size_t* len, size_t n,
+                    hipStream_t st) {
     std::vector<uint64_t> off(n), ln(n);
     size_t total = 0;
     for (size_t i = 0; i < n; ++i) {
@@ -375,78 +528,231 @@ int upload_messages(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, s
     std::vector<uint8_t> packed(total + 8);
     for (size_t i = 0; i < n; ++i)
         if (len[i]) std::memcpy(packed.data() + off[i], msg[i], len[i]);
-    NW_TRY(ctx->w_msg.ensure(total + 8), "ws msg");
-    NW_TRY(ctx->w_msg_off.ensure(n * 8 + 8), "ws msg_off");
-    NW_TRY(ctx->w_msg_len.ensure(n * 8 + 8), "ws msg_len");
-    NW_TRY(hipMemcpyAsync(ctx->w_msg.p, packed.data(), total + 8, hipMemcpyHostToDevice, ctx->stream), "H2D msg");
-    NW_TRY(hipMemcpyAsync(ctx->w_msg_off.p, off.data(), n * 8, hipMemcpyHostToDevice, ctx->stream), "H2D off");
-    NW_TRY(hipMemcpyAsync(ctx->w_msg_len.p, ln.data(), n * 8, hipMemcpyHostToDevice, ctx->stream), "H2D len");
+    NW_TRY(ws->ensure(ws->w_msg, total + 8), "ws msg");
+    NW_TRY(ws->ensure(ws->w_msg_off, n * 8 + 8), "ws msg_off");
+    NW_TRY(ws->ensure(ws->w_msg_len, n * 8 + 8), "ws msg_len");
+    NW_TRY(hipMemcpyAsync(ws->w_msg.p, packed.data(), total + 8, hipMemcpyHostToDevice, st), "H2D msg");
+    NW_TRY(hipMemcpyAsync(ws->w_msg_off.p, off.data(), n * 8, hipMemcpyHostToDevice, st), "H2D off");
+    NW_TRY(hipMemcpyAsync(ws->w_msg_len.p, ln.data(), n * 8, hipMemcpyHostToDevice, st), "H2D len");
+    // pageable sources: make sure the copies have consumed them before the vectors go away
+    NW_TRY(hipStreamSynchronize(st), "sync(messages)");
     return NW_OK;
 }
 
-// Shared body of strict_many / verify_batch: every signature in one "certificate" 0.
+// Strict verify of signatures whose keys are not cached: k_verify_var + k_finish (messages, sigs
+// and raw keys already uploaded to the workspace).
+int enqueue_strict_var(nw_ctx* ctx, Workspace* ws, size_t n, hipStream_t st) {
+    NW_TRY(ws->ensure(ws->w_flags, n * 4 + 4), "ws flags");
+    NW_TRY(ws->ensure(ws->w_sig_cert, n * 4 + 4), "ws sig_cert");
+    NW_TRY(ws->ensure(ws->w_pbuf, n * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
+    NW_TRY(ws->ensure(ws->w_pre, n * 40 + 16), "ws pre");
+    NW_TRY(ws->ensure(ws->w_var, n * 320 * 4 + 16), "ws var table");
+    NW_TRY(hipMemsetAsync(ws->w_sig_cert.p, 0, n * 4 + 4, st), "memset sig_cert");
+    VerifyParams vp{};
+    vp.n = (uint32_t)n;
+    vp.g0 = 0;
+    vp.gn = (uint32_t)n;
+    vp.fk = ctx->finish_k;
+    vp.batch_mode = 0;
+    vp.sig = ws->w_sig.as<uint8_t>();
+    vp.sig_keys = ws->w_keys.as<uint32_t>();
+    vp.sig_cert = ws->w_sig_cert.as<uint32_t>();
+    vp.msg_base = ws->w_msg.as<uint8_t>();
+    vp.msg_off = ws->w_msg_off.as<uint64_t>();
+    vp.msg_len = ws->w_msg_len.as<uint64_t>();
+    vp.btab = ctx->d_btab;
+    vp.flags = ws->w_flags.as<uint32_t>();
+    vp.pbuf = ws->w_pbuf.as<uint32_t>();
+    vp.pre = ws->w_pre.as<uint32_t>();
+    NW_TRY(launch_verify_var(vp, 1, ws->w_var.as<uint32_t>(), st), "k_verify_var");
+    NW_TRY(launch_finish(vp, st), "k_finish");
+    return NW_OK;
+}
+
+// Randomized batch verify of nb consecutive batches (batch b = the next counts[b] signatures)
+// without the key cache: the Pippenger MSM of nw_msm.hip.  Messages, sigs and raw keys are in the
+// workspace.  Writes batch_ok (device, may be null) and/or point_out (device, [nb][40], may be null);
+// bad_out (device, [nb] u32) receives the parse/decode failure flags.
+int enqueue_msm(nw_ctx* ctx, Workspace* ws, size_t nb, const uint32_t* counts, size_t nsig, const uint8_t* zseed,
+                uint64_t batch_base, uint32_t z_off, uint8_t* d_batch_ok, uint32_t* d_point_out, uint32_t** d_bad_out,
+                hipStream_t st) {
+    uint32_t nmax = 0;
+    for (size_t b = 0; b < nb; ++b) nmax = counts[b] > nmax ? counts[b] : nmax;
+    const uint32_t C = nmax >= 512 ? 8 : 7;
+    const uint32_t NA = (uint32_t)msm_nwin_a((int)C), NR = (uint32_t)msm_nwin_r((int)C);
+    const uint32_t B = 1u << (C - 1);
+    std::vector<uint32_t> bfirst(nb), bcount(nb), sig_batch(nsig), wfirst(nb * NA + 1);
+    std::vector<MsmTask> tasks;
+    size_t f = 0;
+    for (size_t b = 0; b < nb; ++b) {
+        bfirst[b] = (uint32_t)f;
+        bcount[b] = counts[b];
+        for (uint32_t t = 0; t < counts[b]; ++t) sig_batch[f + t] = (uint32_t)b;
+        for (uint32_t j = 0; j < NA; ++j) {
+            wfirst[b * NA + j] = (uint32_t)tasks.size();
+            const size_t lo = 2 * f + (j < NR ? 0 : counts[b]), hi = 2 * f + 2 * (size_t)counts[b];
+            for (size_t e = lo; e < hi; e += MSM_CH) {
+                const size_t e1 = e + MSM_CH < hi ? e + MSM_CH : hi;
+                tasks.push_back(MsmTask{(uint32_t)e, (uint32_t)e1, j, (uint32_t)tasks.size()});
+            }
+        }
+        f += counts[b];
+    }
+    wfirst[nb * NA] = (uint32_t)tasks.size();
+    const size_t ntasks = tasks.size();
+    // metadata block: bfirst | bcount | sig_batch | wfirst | tasks | bad | batch verdict scratch
+    const size_t o_bfirst = 0, o_bcount = align256(nb * 4), o_sb = o_bcount + align256(nb * 4),
+                 o_wf = o_sb + align256(nsig * 4 + 4), o_tasks = o_wf + align256(wfirst.size() * 4),
+                 o_bad = o_tasks + align256(ntasks * sizeof(MsmTask) + 16), meta = o_bad + align256(nb * 4);
+    NW_TRY(ws->ensure(ws->w_msm_meta, meta), "ws msm meta");
+    NW_TRY(ws->ensure(ws->w_msm_ent, 2 * nsig * MSM_ENT_WORDS * 4 + 16), "ws msm entries");
+    NW_TRY(ws->ensure(ws->w_msm_dig, (size_t)NA * 2 * nsig * 2 + 16), "ws msm digits");
+    NW_TRY(ws->ensure(ws->w_msm_zs, (size_t)MSM_ZS_WORDS * nsig * 4 + 16), "ws msm zs");
+    NW_TRY(ws->ensure(ws->w_msm_bkt, ntasks * B * MSM_PT_WORDS * 4 + 16), "ws msm buckets");
+    NW_TRY(ws->ensure(ws->w_msm_part, ntasks * 128 * MSM_PT_WORDS * 4 + 16), "ws msm partials");
+    NW_TRY(ws->ensure(ws->w_msm_wpart, (ntasks + nb * NA) * MSM_PT_WORDS * 4 + 16), "ws msm window sums");
+    std::vector<uint8_t> hmeta(meta, 0);
+    std::memcpy(hmeta.data() + o_bfirst, bfirst.data(), nb * 4);
+    std::memcpy(hmeta.data() + o_bcount, bcount.data(), nb * 4);
+    if (nsig) std::memcpy(hmeta.data() + o_sb, sig_batch.data(), nsig * 4);
+    std::memcpy(hmeta.data() + o_wf, wfirst.data(), wfirst.size() * 4);
+    if (ntasks) std::memcpy(hmeta.data() + o_tasks, tasks.data(), ntasks * sizeof(MsmTask));
+    uint8_t* dm = ws->w_msm_meta.as<uint8_t>();
+    NW_TRY(hipMemcpyAsync(dm, hmeta.data(), meta, hipMemcpyHostToDevice, st), "H2D msm meta");
+    NW_TRY(hipStreamSynchronize(st), "sync(msm meta)");   // pageable source
+    MsmParams mp{};
+    mp.nb = (uint32_t)nb;
+    mp.nsig = (uint32_t)nsig;
+    mp.c = C;
+    mp.bfirst = reinterpret_cast<const uint32_t*>(dm + o_bfirst);
+    mp.bcount = reinterpret_cast<const uint32_t*>(dm + o_bcount);
+    mp.sig_batch = reinterpret_cast<const uint32_t*>(dm + o_sb);
+    mp.sig = ws->w_sig.as<uint8_t>();
+    mp.keys = ws->w_keys.as<uint32_t>();
+    mp.msg_base = ws->w_msg.as<uint8_t>();
+    mp.msg_off = ws->w_msg_off.as<uint64_t>();
+    mp.msg_len = ws->w_msg_len.as<uint64_t>();
+    mp.batch_base = batch_base;
+    mp.z_off = z_off;
+    std::memcpy(mp.zseed, zseed, 32);
+    mp.ent = ws->w_msm_ent.as<uint32_t>();
+    mp.dig = ws->w_msm_dig.as<int16_t>();
+    mp.zs = ws->w_msm_zs.as<uint32_t>();
+    mp.bad = reinterpret_cast<uint32_t*>(dm + o_bad);
+    mp.tasks = reinterpret_cast<const MsmTask*>(dm + o_tasks);
+    mp.ntasks = (uint32_t)ntasks;
+    mp.bkt = ws->w_msm_bkt.as<uint32_t>();
+    mp.part = ws->w_msm_part.as<uint32_t>();
+    mp.wpart = ws->w_msm_wpart.as<uint32_t>();
+    mp.wfirst = reinterpret_cast<const uint32_t*>(dm + o_wf);
+    mp.btab = ctx->d_btab;
+    mp.batch_ok = d_batch_ok;
+    mp.point_out = d_point_out;
+    NW_TRY(launch_msm(mp, st), "k_msm");
+    if (d_bad_out) *d_bad_out = mp.bad;
+    return NW_OK;
+}
+
+// Upload per-signature messages, signatures and raw keys to the workspace (uncached-key paths).
+int upload_sig_keys(nw_ctx* ctx, Workspace* ws, const uint8_t* const* msg, const size_t* len,
+                    const uint8_t (*pk)[32], const uint8_t (*sig)[64], size_t n, hipStream_t st) {
+    int rc = upload_messages(ctx, ws, msg, len, n, st);
+    if (rc != NW_OK) return rc;
+    NW_TRY(ws->ensure(ws->w_sig, n * 64 + 64), "ws sig");
+    NW_TRY(ws->ensure(ws->w_keys, n * 32 + 32), "ws keys");
+    NW_TRY(hipMemcpyAsync(ws->w_sig.p, sig, n * 64, hipMemcpyHostToDevice, st), "H2D sig");
+    NW_TRY(hipMemcpyAsync(ws->w_keys.p, pk, n * 32, hipMemcpyHostToDevice, st), "H2D keys");
+    return NW_OK;
+}
+
+// Shared body of strict_many / verify_batch: every signature in one "certificate" 0.  Cached keys
+// take the comb path; a call with any key outside the cache takes the variable-base path (strict:
+// k_verify_var; batch: the MSM) and leaves the cache unchanged.
 int run_generic(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const uint8_t (*pk)[32],
                 const uint8_t (*sig)[64], size_t n, const uint8_t* zseed, uint64_t batch_index, uint32_t batch_mode,
                 uint8_t* ok_out, uint8_t* verdict_out) {
-    std::vector<uint32_t> slots(n);
-    int rc = ensure_slots(ctx, pk, nullptr, n, slots.data());
-    if (rc != NW_OK) return rc;
-    rc = upload_messages(ctx, msg, len, n);
-    if (rc != NW_OK) return rc;
-    NW_TRY(ctx->w_sig.ensure(n * 64), "ws sig");
-    NW_TRY(ctx->w_signer.ensure(n * 4), "ws signer");
-    NW_TRY(ctx->w_cert_first.ensure(16), "ws first");
-    NW_TRY(ctx->w_cert_n.ensure(16), "ws n");
-    NW_TRY(ctx->w_cert_ok.ensure(16), "ws cert_ok");
-    NW_TRY(ctx->w_ok.ensure(n + 16), "ws ok");
-    const uint32_t first = 0, nv = (uint32_t)n;
-    NW_TRY(hipMemcpyAsync(ctx->w_sig.p, sig, n * 64, hipMemcpyHostToDevice, ctx->stream), "H2D sig");
-    NW_TRY(hipMemcpyAsync(ctx->w_signer.p, slots.data(), n * 4, hipMemcpyHostToDevice, ctx->stream), "H2D signer");
-    NW_TRY(hipMemcpyAsync(ctx->w_cert_first.p, &first, 4, hipMemcpyHostToDevice, ctx->stream), "H2D first");
-    NW_TRY(hipMemcpyAsync(ctx->w_cert_n.p, &nv, 4, hipMemcpyHostToDevice, ctx->stream), "H2D n");
-    rc = enqueue_certs(ctx, 1, ctx->w_cert_first.as<uint32_t>(), ctx->w_cert_n.as<uint32_t>(), n,
-                       ctx->w_sig.as<uint8_t>(), ctx->w_signer.as<uint32_t>(), 1, nullptr, ctx->w_msg.as<uint8_t>(),
-                       ctx->w_msg_off.as<uint64_t>(), ctx->w_msg_len.as<uint64_t>(), zseed, batch_index, batch_mode,
-                       ctx->w_cert_ok.as<uint8_t>(), nullptr, nullptr, ctx->stream);
-    if (rc != NW_OK) return rc;
-    if (ok_out) {
-        NW_TRY(launch_flags_to_ok((uint32_t)n, ctx->w_flags.as<uint32_t>(), ctx->w_ok.as<uint8_t>(), ctx->stream),
-               "k_flags_to_ok");
-        NW_TRY(hipMemcpyAsync(ok_out, ctx->w_ok.p, n, hipMemcpyDeviceToHost, ctx->stream), "D2H ok");
+    std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);
+    Lease lease(ctx);
+    Workspace* ws = lease.ws();
+    if (!ws) {
+        set_error(ctx, "workspace allocation failed");
+        return NW_ERR_DEVICE;
     }
-    if (verdict_out) NW_TRY(hipMemcpyAsync(verdict_out, ctx->w_cert_ok.p, 1, hipMemcpyDeviceToHost, ctx->stream), "D2H");
-    NW_TRY(hipStreamSynchronize(ctx->stream), "sync");
+    hipStream_t st = ws->stream;
+    NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
+    std::vector<uint32_t> slots(n);
+    const bool cached = lookup_slots(ctx, pk, n, slots.data());
+    int rc = NW_OK;
+    if (!cached) {
+        rc = upload_sig_keys(ctx, ws, msg, len, pk, sig, n, st);
+        if (rc != NW_OK) return rc;
+        NW_TRY(ws->ensure(ws->w_ok, n + 16), "ws ok");
+        if (batch_mode) {
+            NW_TRY(ws->ensure(ws->w_cert_ok, 16), "ws verdict");
+            const uint32_t cnt = (uint32_t)n;
+            rc = enqueue_msm(ctx, ws, 1, &cnt, n, zseed, batch_index, 0, ws->w_cert_ok.as<uint8_t>(), nullptr, nullptr,
+                             st);
+            if (rc != NW_OK) return rc;
+        } else {
+            rc = enqueue_strict_var(ctx, ws, n, st);
+            if (rc != NW_OK) return rc;
+        }
+    } else {
+        rc = upload_messages(ctx, ws, msg, len, n, st);
+        if (rc != NW_OK) return rc;
+        NW_TRY(ws->ensure(ws->w_sig, n * 64), "ws sig");
+        NW_TRY(ws->ensure(ws->w_signer, n * 4), "ws signer");
+        NW_TRY(ws->ensure(ws->w_cert_first, 16), "ws first");
+        NW_TRY(ws->ensure(ws->w_cert_n, 16), "ws n");
+        NW_TRY(ws->ensure(ws->w_cert_ok, 16), "ws cert_ok");
+        NW_TRY(ws->ensure(ws->w_ok, n + 16), "ws ok");
+        const uint32_t first = 0, nv = (uint32_t)n;
+        NW_TRY(hipMemcpyAsync(ws->w_sig.p, sig, n * 64, hipMemcpyHostToDevice, st), "H2D sig");
+        NW_TRY(hipMemcpyAsync(ws->w_signer.p, slots.data(), n * 4, hipMemcpyHostToDevice, st), "H2D signer");
+        NW_TRY(hipMemcpyAsync(ws->w_cert_first.p, &first, 4, hipMemcpyHostToDevice, st), "H2D first");
+        NW_TRY(hipMemcpyAsync(ws->w_cert_n.p, &nv, 4, hipMemcpyHostToDevice, st), "H2D n");
+        rc = enqueue_certs(ctx, ws, 1, ws->w_cert_first.as<uint32_t>(), ws->w_cert_n.as<uint32_t>(), n,
+                           ws->w_sig.as<uint8_t>(), ws->w_signer.as<uint32_t>(), 1, nullptr, ws->w_msg.as<uint8_t>(),
+                           ws->w_msg_off.as<uint64_t>(), ws->w_msg_len.as<uint64_t>(), zseed, batch_index, batch_mode,
+                           ws->w_cert_ok.as<uint8_t>(), nullptr, nullptr, st);
+        if (rc != NW_OK) return rc;
+    }
+    if (ok_out) {
+        NW_TRY(launch_flags_to_ok((uint32_t)n, ws->w_flags.as<uint32_t>(), ws->w_ok.as<uint8_t>(), st),
+               "k_flags_to_ok");
+        NW_TRY(hipMemcpyAsync(ok_out, ws->w_ok.p, n, hipMemcpyDeviceToHost, st), "D2H ok");
+    }
+    if (verdict_out) NW_TRY(hipMemcpyAsync(verdict_out, ws->w_cert_ok.p, 1, hipMemcpyDeviceToHost, st), "D2H");
+    NW_TRY(hipStreamSynchronize(st), "sync");
+    lease.synced();
     return NW_OK;
+}
+
+bool zseed_ok(nw_ctx* ctx, const uint8_t* zseed) {
+    if (zseed) return true;
+    set_error(ctx, "zseed is NULL: batch coefficients need a fresh 32-byte CSPRNG seed per call");
+    return false;
 }
 
 }  // namespace
 
 extern "C" {
 
-const char* nw_version(void) { return "nwcrypto 0.1 gfx950 " __DATE__; }
+const char* nw_version(void) { return "nwcrypto 0.2 gfx950 " __DATE__; }
 
 int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     if (!out) return NW_ERR_ARG;
     *out = nullptr;
-    nw_ctx* ctx = new nw_ctx();
     int ndev = 0;
     hipError_t e = hipGetDeviceCount(&ndev);
-    if (e != hipSuccess || ndev == 0) {
-        delete ctx;
-        return NW_ERR_DEVICE;
-    }
+    if (e != hipSuccess || ndev == 0) return NW_ERR_DEVICE;
     int dev = opts && opts->device >= 0 ? opts->device : -1;
-    if (dev < 0) {
-        e = hipGetDevice(&dev);
-        if (e != hipSuccess) {
-            delete ctx;
-            return NW_ERR_DEVICE;
-        }
-    }
-    if (dev >= ndev) {
-        delete ctx;
+    if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_DEVICE;
+    if (dev >= ndev) return NW_ERR_ARG;
+    if (opts && opts->key_window && opts->key_window != -1 && opts->key_window != 8 && opts->key_window != 12 &&
+        opts->key_window != 16 && opts->key_window != 20)
         return NW_ERR_ARG;
-    }
+    nw_ctx* ctx = new nw_ctx();
     ctx->device = dev;
     ctx->finish_k = finish_k();
     if (opts && opts->max_keys) {
@@ -454,11 +760,6 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
         ctx->max_keys_user = true;
     }
     if (opts && opts->key_window) {
-        if (opts->key_window != -1 && opts->key_window != 8 && opts->key_window != 12 && opts->key_window != 16 &&
-            opts->key_window != 20) {
-            delete ctx;
-            return NW_ERR_ARG;
-        }
         ctx->key_window = opts->key_window;
         if (ctx->key_window > 0) fix_window(ctx, 0);
     }
@@ -471,13 +772,14 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     uint32_t* d_binfo = nullptr;
     if (hipMalloc(&ctx->d_btab, comb_words(B_WINDOW) * 4) != hipSuccess || hipMalloc(&d_braw, 32) != hipSuccess ||
         hipMalloc(&d_binfo, 16) != hipSuccess) {
+        if (d_braw) (void)hipFree(d_braw);
         nw_ctx_destroy(ctx);
         return NW_ERR_NOMEM;
     }
     int rc = NW_OK;
     if (hipMemcpy(d_braw, kBaseEnc, 32, hipMemcpyHostToDevice) != hipSuccess) rc = NW_ERR_DEVICE;
     if (rc == NW_OK) rc = build_keys(ctx, d_braw, d_binfo, ctx->d_btab, 1, B_WINDOW);
-    if (rc == NW_OK && hipStreamSynchronize(ctx->stream) != hipSuccess) rc = NW_ERR_DEVICE;
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == NW_OK) rc = NW_ERR_DEVICE;
     (void)hipFree(d_braw);
     (void)hipFree(d_binfo);
     if (rc != NW_OK) {
@@ -492,18 +794,18 @@ void nw_ctx_destroy(nw_ctx* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    for (DevBuf* b : {&ctx->w_bases, &ctx->w_sig, &ctx->w_signer, &ctx->w_sig_cert, &ctx->w_cert_first, &ctx->w_cert_n,
-                      &ctx->w_msg, &ctx->w_msg_off, &ctx->w_msg_len, &ctx->w_flags, &ctx->w_slow_count,
-                      &ctx->w_slow_list, &ctx->w_slow_slot, &ctx->w_slow_buf, &ctx->w_cert_ok, &ctx->w_stake_out,
-                      &ctx->w_ok, &ctx->w_misc, &ctx->w_out, &ctx->w_pbuf, &ctx->w_pre,
-                      &ctx->w_counts, &ctx->w_cursor, &ctx->w_perm, &ctx->w_io})
-        b->release();
-    ctx->h_io.release();
+    for (auto& w : ctx->pool) {
+        if (w->pending) (void)hipEventSynchronize(w->done);
+        if (w->stream) (void)hipStreamSynchronize(w->stream);
+        w->release_all();
+        if (w->done) (void)hipEventDestroy(w->done);
+        if (w->stream) (void)hipStreamDestroy(w->stream);
+    }
+    ctx->w_bases.release();
     for (auto& ev : ctx->prof_events) {
         (void)hipEventDestroy(ev.first);
         (void)hipEventDestroy(ev.second);
     }
-
     for (uint32_t* p : {ctx->d_btab, ctx->d_keys_raw, ctx->d_key_info, ctx->d_stake, ctx->d_key_tab})
         if (p) (void)hipFree(p);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -512,7 +814,7 @@ void nw_ctx_destroy(nw_ctx* ctx) {
 
 int nw_profile_enable(nw_ctx* ctx, int on) {
     if (!ctx) return NW_ERR_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    std::lock_guard<std::mutex> g(ctx->prof_mu);
     ctx->prof_on = on != 0;
     return NW_OK;
 }
@@ -523,8 +825,8 @@ int nw_profile_read(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launc
 
 int nw_profile_read_sigs(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launches, uint64_t* verify_sigs) {
     if (!ctx) return NW_ERR_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    std::lock_guard<std::mutex> g(ctx->prof_mu);
     double total = 0;
     for (size_t i = 0; i < ctx->prof_used; ++i) {
         NW_TRY(hipEventSynchronize(ctx->prof_events[i].second), "hipEventSynchronize");
@@ -540,21 +842,32 @@ int nw_profile_read_sigs(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_
     return NW_OK;
 }
 
-const char* nw_last_error(const nw_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+const char* nw_last_error(const nw_ctx* ctx) {
+    (void)ctx;
+    return tl_last_error.c_str();
+}
 
-size_t nw_committee_size(const nw_ctx* ctx) { return ctx ? ctx->nkeys : 0; }
+size_t nw_committee_size(const nw_ctx* ctx) {
+    if (!ctx) return 0;
+    std::shared_lock<std::shared_mutex> g(const_cast<nw_ctx*>(ctx)->keys_mu);
+    return ctx->nkeys;
+}
 
-int nw_key_window(const nw_ctx* ctx) { return ctx ? ctx->key_window : 0; }
+int nw_key_window(const nw_ctx* ctx) {
+    if (!ctx) return 0;
+    std::shared_lock<std::shared_mutex> g(const_cast<nw_ctx*>(ctx)->keys_mu);
+    return ctx->key_window;
+}
 
 int nw_base_window(void) { return B_WINDOW; }
 
 int nw_committee_load(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, size_t n, uint32_t* slot_out) {
     if (!ctx || (!pk && n)) return NW_ERR_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    std::unique_lock<std::shared_mutex> g(ctx->keys_mu);
     std::vector<uint32_t> slots(n);
     int rc = ensure_slots(ctx, pk, stake, n, slots.data());
-    if (rc == NW_OK && slot_out) std::memcpy(slot_out, slots.data(), n * 4);
+    if (rc == NW_OK && slot_out && n) std::memcpy(slot_out, slots.data(), n * 4);
     return rc;
 }
 
@@ -562,7 +875,7 @@ int nw_verify_strict_many(nw_ctx* ctx, const uint8_t* const* msg, const size_t* 
                           const uint8_t (*sig)[64], size_t n, uint8_t* ok) {
     if (!ctx || !ok || (n && (!msg || !len || !pk || !sig))) return NW_ERR_ARG;
     if (n == 0) return NW_OK;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n > 0xFFFFFFF0u) return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
     return run_generic(ctx, msg, len, pk, sig, n, nullptr, 0, 0, ok, nullptr);
 }
@@ -580,8 +893,9 @@ int nw_verify_strict(nw_ctx* ctx, const uint8_t* msg, size_t len, const uint8_t 
 int nw_verify_batch(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const uint8_t (*pk)[32],
                     const uint8_t (*sig)[64], size_t n, const uint8_t zseed[32], uint64_t batch_index) {
     if (!ctx || (n && (!msg || !len || !pk || !sig))) return NW_ERR_ARG;
+    if (!zseed_ok(ctx, zseed)) return NW_ERR_ARG;
     if (n == 0) return NW_OK;   // empty batch: the MSM is (-0)B = identity -> Ok
-    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n > 0xFFFFFFF0u) return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
     uint8_t verdict = 0;
     int rc = run_generic(ctx, msg, len, pk, sig, n, zseed, batch_index, 1, nullptr, &verdict);
@@ -589,11 +903,89 @@ int nw_verify_batch(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, c
     return verdict ? NW_OK : NW_ERR_SIG;
 }
 
+int nw_verify_batches_pk(nw_ctx* ctx, size_t nb, const uint32_t* counts, const uint8_t* const* msg,
+                         const size_t* len, const uint8_t (*pk)[32], const uint8_t (*sig)[64],
+                         const uint8_t zseed[32], uint64_t batch_base, uint8_t* batch_ok) {
+    if (!ctx || (nb && (!counts || !batch_ok))) return NW_ERR_ARG;
+    if (!zseed_ok(ctx, zseed)) return NW_ERR_ARG;
+    size_t nsig = 0;
+    for (size_t b = 0; b < nb; ++b) nsig += counts[b];
+    if (nsig && (!msg || !len || !pk || !sig)) return NW_ERR_ARG;
+    if (nsig > 0x7FFFFFF0u) return NW_ERR_ARG;
+    if (nb == 0) return NW_OK;
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);
+    Lease lease(ctx);
+    Workspace* ws = lease.ws();
+    if (!ws) return NW_ERR_DEVICE;
+    hipStream_t st = ws->stream;
+    NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
+    int rc = upload_sig_keys(ctx, ws, msg, len, pk, sig, nsig, st);
+    if (rc != NW_OK) return rc;
+    NW_TRY(ws->ensure(ws->w_cert_ok, nb + 16), "ws verdicts");
+    rc = enqueue_msm(ctx, ws, nb, counts, nsig, zseed, batch_base, 0, ws->w_cert_ok.as<uint8_t>(), nullptr, nullptr,
+                     st);
+    if (rc != NW_OK) return rc;
+    NW_TRY(hipMemcpyAsync(batch_ok, ws->w_cert_ok.p, nb, hipMemcpyDeviceToHost, st), "D2H verdicts");
+    NW_TRY(hipStreamSynchronize(st), "sync");
+    lease.synced();
+    return NW_OK;
+}
+
+int nw_verify_batch_partial(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const uint8_t (*pk)[32],
+                            const uint8_t (*sig)[64], size_t n, const uint8_t zseed[32], uint64_t batch_index,
+                            uint32_t z_offset, uint8_t point[NW_POINT_BYTES], int* bad) {
+    if (!ctx || !point || !bad || (n && (!msg || !len || !pk || !sig))) return NW_ERR_ARG;
+    if (!zseed_ok(ctx, zseed)) return NW_ERR_ARG;
+    if (n > 0x7FFFFFF0u) return NW_ERR_ARG;
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);
+    Lease lease(ctx);
+    Workspace* ws = lease.ws();
+    if (!ws) return NW_ERR_DEVICE;
+    hipStream_t st = ws->stream;
+    NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
+    int rc = upload_sig_keys(ctx, ws, msg, len, pk, sig, n, st);
+    if (rc != NW_OK) return rc;
+    NW_TRY(ws->ensure(ws->w_out, MSM_PT_WORDS * 4 + 16), "ws point");
+    const uint32_t cnt = (uint32_t)n;
+    uint32_t* d_bad = nullptr;
+    rc = enqueue_msm(ctx, ws, 1, &cnt, n, zseed, batch_index, z_offset, nullptr, ws->w_out.as<uint32_t>(), &d_bad, st);
+    if (rc != NW_OK) return rc;
+    uint32_t hbad = 0;
+    NW_TRY(hipMemcpyAsync(point, ws->w_out.p, NW_POINT_BYTES, hipMemcpyDeviceToHost, st), "D2H point");
+    NW_TRY(hipMemcpyAsync(&hbad, d_bad, 4, hipMemcpyDeviceToHost, st), "D2H bad");
+    NW_TRY(hipStreamSynchronize(st), "sync");
+    lease.synced();
+    *bad = hbad ? 1 : 0;
+    return NW_OK;
+}
+
+int nw_points_sum_is_identity(nw_ctx* ctx, const uint8_t (*points)[NW_POINT_BYTES], size_t k, int* is_identity) {
+    if (!ctx || !is_identity || (k && !points)) return NW_ERR_ARG;
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    Lease lease(ctx);
+    Workspace* ws = lease.ws();
+    if (!ws) return NW_ERR_DEVICE;
+    hipStream_t st = ws->stream;
+    NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
+    NW_TRY(ws->ensure(ws->w_misc, k * NW_POINT_BYTES + 64), "ws points");
+    if (k) NW_TRY(hipMemcpyAsync(ws->w_misc.p, points, k * NW_POINT_BYTES, hipMemcpyHostToDevice, st), "H2D points");
+    uint8_t* d_out = ws->w_misc.as<uint8_t>() + k * NW_POINT_BYTES;
+    NW_TRY(launch_msm_points_identity((uint32_t)k, ws->w_misc.as<uint32_t>(), d_out, st), "k_points_identity");
+    uint8_t r = 0;
+    NW_TRY(hipMemcpyAsync(&r, d_out, 1, hipMemcpyDeviceToHost, st), "D2H");
+    NW_TRY(hipStreamSynchronize(st), "sync");
+    lease.synced();
+    *is_identity = r ? 1 : 0;
+    return NW_OK;
+}
+
 int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint8_t (*sig)[64],
                     const uint32_t* signer_slot, const uint8_t (*msg)[32], const uint8_t zseed[32], uint64_t cert_base,
                     uint8_t* cert_ok, uint8_t* sig_ok, uint64_t* accepted_stake) {
     if (!ctx || (ncerts && (!certs || !msg))) return NW_ERR_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!zseed_ok(ctx, zseed)) return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
     size_t nsigs = 0;
     std::vector<uint32_t> first(ncerts), nv(ncerts);
@@ -603,49 +995,54 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
         const size_t end = (size_t)certs[c].first_vote + certs[c].n_votes;
         if (end > nsigs) nsigs = end;
     }
+    if (nsigs > 0xFFFFFFF0u) return NW_ERR_ARG;
     if (nsigs && (!sig || !signer_slot)) return NW_ERR_ARG;
+    std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);
     for (size_t v = 0; v < nsigs; ++v)
         if (signer_slot[v] >= ctx->nkeys) {
-            ctx->last_error = "signer slot out of range (load the committee first)";
+            set_error(ctx, "signer slot out of range (load the committee first)");
             return NW_ERR_ARG;
         }
     if (ncerts == 0) return NW_OK;   // nothing to verify (nsigs is 0 too)
+    Lease lease(ctx);
+    Workspace* ws = lease.ws();
+    if (!ws) return NW_ERR_DEVICE;
+    hipStream_t st = ws->stream;
+    NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
     // one staged H2D of every input and one D2H of every output (single-certificate latency)
     const size_t o_sig = 0, o_signer = align256(o_sig + nsigs * 64), o_first = align256(o_signer + nsigs * 4),
                  o_nv = align256(o_first + ncerts * 4), o_msg = align256(o_nv + ncerts * 4),
                  in_bytes = align256(o_msg + ncerts * 32);
     const size_t o_cok = 0, o_stake = align256(ncerts), o_ok = align256(o_stake + ncerts * 8),
                  out_bytes = align256(o_ok + nsigs);
-    NW_TRY(ctx->w_io.ensure(in_bytes + out_bytes), "ws io");
-    NW_TRY(ctx->h_io.ensure(in_bytes > out_bytes ? in_bytes : out_bytes), "pinned io");
-    uint8_t* h = ctx->h_io.bytes();
+    NW_TRY(ws->ensure(ws->w_io, in_bytes + out_bytes), "ws io");
+    NW_TRY(ws->h_io.ensure(in_bytes > out_bytes ? in_bytes : out_bytes), "pinned io");
+    uint8_t* h = ws->h_io.bytes();
     if (nsigs) {
         std::memcpy(h + o_sig, sig, nsigs * 64);
         std::memcpy(h + o_signer, signer_slot, nsigs * 4);
     }
-    if (ncerts) {
-        std::memcpy(h + o_first, first.data(), ncerts * 4);
-        std::memcpy(h + o_nv, nv.data(), ncerts * 4);
-        std::memcpy(h + o_msg, msg, ncerts * 32);
-    }
-    uint8_t* d_in = ctx->w_io.as<uint8_t>();
+    std::memcpy(h + o_first, first.data(), ncerts * 4);
+    std::memcpy(h + o_nv, nv.data(), ncerts * 4);
+    std::memcpy(h + o_msg, msg, ncerts * 32);
+    uint8_t* d_in = ws->w_io.as<uint8_t>();
     uint8_t* d_out = d_in + in_bytes;
-    hipStream_t st = ctx->stream;
     NW_TRY(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, st), "H2D inputs");
-    int rc = enqueue_certs(ctx, ncerts, reinterpret_cast<const uint32_t*>(d_in + o_first),
+    int rc = enqueue_certs(ctx, ws, ncerts, reinterpret_cast<const uint32_t*>(d_in + o_first),
                            reinterpret_cast<const uint32_t*>(d_in + o_nv), nsigs, d_in + o_sig,
                            reinterpret_cast<const uint32_t*>(d_in + o_signer), 0, d_in + o_msg, nullptr, nullptr,
                            nullptr, zseed, cert_base, 1, d_out + o_cok, nullptr,
                            reinterpret_cast<uint64_t*>(d_out + o_stake), st);
-    if (rc != NW_OK) return rc;
+    if (rc != NW_OK) return rc;   // the lease synchronizes the stream (the H2D may be in flight)
     if (sig_ok && nsigs)
-        NW_TRY(launch_flags_to_ok((uint32_t)nsigs, ctx->w_flags.as<uint32_t>(), d_out + o_ok, st), "k_flags_to_ok");
+        NW_TRY(launch_flags_to_ok((uint32_t)nsigs, ws->w_flags.as<uint32_t>(), d_out + o_ok, st), "k_flags_to_ok");
     // the H2D above has completed in stream order before this copy overwrites the staging buffer
     NW_TRY(hipMemcpyAsync(h, d_out, out_bytes, hipMemcpyDeviceToHost, st), "D2H outputs");
     NW_TRY(hipStreamSynchronize(st), "sync");
+    lease.synced();
     if (sig_ok && nsigs) std::memcpy(sig_ok, h + o_ok, nsigs);
-    if (cert_ok && ncerts) std::memcpy(cert_ok, h + o_cok, ncerts);
-    if (accepted_stake && ncerts) std::memcpy(accepted_stake, h + o_stake, ncerts * 8);
+    if (cert_ok) std::memcpy(cert_ok, h + o_cok, ncerts);
+    if (accepted_stake) std::memcpy(accepted_stake, h + o_stake, ncerts * 8);
     return NW_OK;
 }
 
@@ -654,67 +1051,108 @@ int nw_verify_batches(nw_ctx* ctx, size_t nb, const uint32_t* first, const uint3
                       const uint8_t (*sig)[64], const uint8_t zseed[32], uint64_t batch_base, uint8_t* batch_ok,
                       uint8_t* sig_ok) {
     if (!ctx || (nb && (!first || !nvotes))) return NW_ERR_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!zseed_ok(ctx, zseed)) return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
     size_t nsigs = 0;
     for (size_t b = 0; b < nb; ++b) {
         const size_t end = (size_t)first[b] + nvotes[b];
         if (end > nsigs) nsigs = end;
     }
+    if (nsigs > 0xFFFFFFF0u) return NW_ERR_ARG;
     if (nsigs && (!sig || !signer_slot || !msg || !len)) return NW_ERR_ARG;
+    std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);
     for (size_t v = 0; v < nsigs; ++v)
         if (signer_slot[v] >= ctx->nkeys) {
-            ctx->last_error = "signer slot out of range (load the keys first)";
+            set_error(ctx, "signer slot out of range (load the keys first)");
             return NW_ERR_ARG;
         }
-    hipStream_t st = ctx->stream;
-    int rc = upload_messages(ctx, msg, len, nsigs);
+    Lease lease(ctx);
+    Workspace* ws = lease.ws();
+    if (!ws) return NW_ERR_DEVICE;
+    hipStream_t st = ws->stream;
+    NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
+    int rc = upload_messages(ctx, ws, msg, len, nsigs, st);
     if (rc != NW_OK) return rc;
-    NW_TRY(ctx->w_sig.ensure(nsigs * 64 + 64), "ws sig");
-    NW_TRY(ctx->w_signer.ensure(nsigs * 4 + 4), "ws signer");
-    NW_TRY(ctx->w_cert_first.ensure(nb * 4 + 4), "ws first");
-    NW_TRY(ctx->w_cert_n.ensure(nb * 4 + 4), "ws n");
-    NW_TRY(ctx->w_cert_ok.ensure(nb + 16), "ws batch_ok");
-    NW_TRY(ctx->w_ok.ensure(nsigs + 16), "ws ok");
+    NW_TRY(ws->ensure(ws->w_sig, nsigs * 64 + 64), "ws sig");
+    NW_TRY(ws->ensure(ws->w_signer, nsigs * 4 + 4), "ws signer");
+    NW_TRY(ws->ensure(ws->w_cert_first, nb * 4 + 4), "ws first");
+    NW_TRY(ws->ensure(ws->w_cert_n, nb * 4 + 4), "ws n");
+    NW_TRY(ws->ensure(ws->w_cert_ok, nb + 16), "ws batch_ok");
+    NW_TRY(ws->ensure(ws->w_ok, nsigs + 16), "ws ok");
     if (nsigs) {
-        NW_TRY(hipMemcpyAsync(ctx->w_sig.p, sig, nsigs * 64, hipMemcpyHostToDevice, st), "H2D sig");
-        NW_TRY(hipMemcpyAsync(ctx->w_signer.p, signer_slot, nsigs * 4, hipMemcpyHostToDevice, st), "H2D signer");
+        NW_TRY(hipMemcpyAsync(ws->w_sig.p, sig, nsigs * 64, hipMemcpyHostToDevice, st), "H2D sig");
+        NW_TRY(hipMemcpyAsync(ws->w_signer.p, signer_slot, nsigs * 4, hipMemcpyHostToDevice, st), "H2D signer");
     }
     if (nb) {
-        NW_TRY(hipMemcpyAsync(ctx->w_cert_first.p, first, nb * 4, hipMemcpyHostToDevice, st), "H2D first");
-        NW_TRY(hipMemcpyAsync(ctx->w_cert_n.p, nvotes, nb * 4, hipMemcpyHostToDevice, st), "H2D n");
+        NW_TRY(hipMemcpyAsync(ws->w_cert_first.p, first, nb * 4, hipMemcpyHostToDevice, st), "H2D first");
+        NW_TRY(hipMemcpyAsync(ws->w_cert_n.p, nvotes, nb * 4, hipMemcpyHostToDevice, st), "H2D n");
     }
-    rc = enqueue_certs(ctx, nb, ctx->w_cert_first.as<uint32_t>(), ctx->w_cert_n.as<uint32_t>(), nsigs,
-                       ctx->w_sig.as<uint8_t>(), ctx->w_signer.as<uint32_t>(), 1, nullptr, ctx->w_msg.as<uint8_t>(),
-                       ctx->w_msg_off.as<uint64_t>(), ctx->w_msg_len.as<uint64_t>(), zseed, batch_base, 1,
-                       ctx->w_cert_ok.as<uint8_t>(), nullptr, nullptr, st);
+    rc = enqueue_certs(ctx, ws, nb, ws->w_cert_first.as<uint32_t>(), ws->w_cert_n.as<uint32_t>(), nsigs,
+                       ws->w_sig.as<uint8_t>(), ws->w_signer.as<uint32_t>(), 1, nullptr, ws->w_msg.as<uint8_t>(),
+                       ws->w_msg_off.as<uint64_t>(), ws->w_msg_len.as<uint64_t>(), zseed, batch_base, 1,
+                       ws->w_cert_ok.as<uint8_t>(), nullptr, nullptr, st);
     if (rc != NW_OK) return rc;
     if (sig_ok && nsigs) {
-        NW_TRY(launch_flags_to_ok((uint32_t)nsigs, ctx->w_flags.as<uint32_t>(), ctx->w_ok.as<uint8_t>(), st),
+        NW_TRY(launch_flags_to_ok((uint32_t)nsigs, ws->w_flags.as<uint32_t>(), ws->w_ok.as<uint8_t>(), st),
                "k_flags_to_ok");
-        NW_TRY(hipMemcpyAsync(sig_ok, ctx->w_ok.p, nsigs, hipMemcpyDeviceToHost, st), "D2H sig_ok");
+        NW_TRY(hipMemcpyAsync(sig_ok, ws->w_ok.p, nsigs, hipMemcpyDeviceToHost, st), "D2H sig_ok");
     }
-    if (batch_ok && nb) NW_TRY(hipMemcpyAsync(batch_ok, ctx->w_cert_ok.p, nb, hipMemcpyDeviceToHost, st), "D2H");
+    if (batch_ok && nb) NW_TRY(hipMemcpyAsync(batch_ok, ws->w_cert_ok.p, nb, hipMemcpyDeviceToHost, st), "D2H");
     NW_TRY(hipStreamSynchronize(st), "sync");
+    lease.synced();
     return NW_OK;
 }
 
 int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first, const uint32_t* d_cert_nvotes,
                         size_t nsigs, const uint8_t* d_sig64, const uint32_t* d_signer_slot, const uint8_t* d_msg32,
                         const uint8_t zseed[32], uint64_t cert_base, uint8_t* d_cert_ok, uint32_t* d_sig_flags,
-                        uint64_t* d_accepted_stake, void* stream) {
+                        uint64_t* d_accepted_stake, uint32_t* d_status, void* stream) {
     if (!ctx) return NW_ERR_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!zseed_ok(ctx, zseed)) return NW_ERR_ARG;
+    if (ncerts > 0xFFFFFFF0u || nsigs > 0xFFFFFFF0u) return NW_ERR_ARG;
+    if ((ncerts && (!d_cert_first || !d_cert_nvotes || !d_msg32)) || (nsigs && (!d_sig64 || !d_signer_slot)))
+        return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
-    return enqueue_certs(ctx, ncerts, d_cert_first, d_cert_nvotes, nsigs, d_sig64, d_signer_slot, 0, d_msg32, nullptr,
-                         nullptr, nullptr, zseed, cert_base, 1, d_cert_ok, d_sig_flags, d_accepted_stake,
-                         reinterpret_cast<hipStream_t>(stream));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);
+    Lease lease(ctx);
+    Workspace* ws = lease.ws();
+    if (!ws) return NW_ERR_DEVICE;
+    NW_TRY(lease.bind(st, false), "hipStreamWaitEvent");
+    // input validation on the device (the inputs are device-resident); every kernel below also
+    // clamps them, so invalid inputs never fault
+    uint32_t* status = d_status;
+    if (!status) {
+        NW_TRY(ws->ensure(ws->w_status, 16), "ws status");
+        status = ws->w_status.as<uint32_t>();
+    }
+    NW_TRY(hipMemsetAsync(status, 0, 4, st), "memset status");
+    NW_TRY(launch_validate_certs((uint32_t)ncerts, (uint32_t)nsigs, (uint32_t)ctx->nkeys, d_cert_first,
+                                 d_cert_nvotes, d_signer_slot, status, st),
+           "k_validate_certs");
+    if (!d_status) {   // synchronous validation: NW_ERR_ARG before any verification is enqueued
+        NW_TRY(ws->h_io.ensure(16), "pinned status");
+        NW_TRY(hipMemcpyAsync(ws->h_io.p, status, 4, hipMemcpyDeviceToHost, st), "D2H status");
+        NW_TRY(hipStreamSynchronize(st), "sync(status)");
+        uint32_t sv = 0;
+        std::memcpy(&sv, ws->h_io.p, 4);
+        if (sv != 0) {
+            set_error(ctx, "nw_verify_certs_dev: vote range past nsigs or signer slot outside the key cache");
+            lease.synced();
+            return NW_ERR_ARG;
+        }
+    }
+    int rc = enqueue_certs(ctx, ws, ncerts, d_cert_first, d_cert_nvotes, nsigs, d_sig64, d_signer_slot, 0, d_msg32,
+                           nullptr, nullptr, nullptr, zseed, cert_base, 1, d_cert_ok, d_sig_flags, d_accepted_stake,
+                           st);
+    NW_TRY(lease.finish(), "hipEventRecord");
+    return rc;
 }
 
 int nw_sha512_many_dev(nw_ctx* ctx, const uint8_t* d_base, const uint64_t* d_off, const uint64_t* d_len, size_t n,
                        uint8_t* d_out64, void* stream) {
-    if (!ctx) return NW_ERR_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    if (!ctx || (n && (!d_base || !d_off || !d_len || !d_out64))) return NW_ERR_ARG;
+    if (n > 0xFFFFFFF0u) return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
     NW_TRY(launch_sha512_many((uint32_t)n, d_base, d_off, d_len, d_out64, reinterpret_cast<hipStream_t>(stream)),
            "k_sha512_many");
@@ -725,7 +1163,7 @@ int nw_sha512_many(nw_ctx* ctx, const uint8_t* base, const uint64_t* off, const 
                    uint8_t (*out)[64]) {
     if (!ctx || (n && (!off || !len || !out))) return NW_ERR_ARG;
     if (n == 0) return NW_OK;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n > 0xFFFFFFF0u) return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
     // upload only the referenced span
     uint64_t lo = UINT64_MAX, hi = 0;
@@ -734,22 +1172,28 @@ int nw_sha512_many(nw_ctx* ctx, const uint8_t* base, const uint64_t* off, const 
         if (off[i] + len[i] > hi) hi = off[i] + len[i];
     }
     if (hi < lo) hi = lo;
+    if (hi > lo && !base) return NW_ERR_ARG;
     std::vector<uint64_t> roff(n);
     for (size_t i = 0; i < n; ++i) roff[i] = off[i] - lo;
     const size_t span = (size_t)(hi - lo);
-    hipStream_t st = ctx->stream;
-    NW_TRY(ctx->w_msg.ensure(span + 16), "ws msg");
-    NW_TRY(ctx->w_msg_off.ensure(n * 8), "ws off");
-    NW_TRY(ctx->w_msg_len.ensure(n * 8), "ws len");
-    NW_TRY(ctx->w_out.ensure(n * 64), "ws out");
-    if (span) NW_TRY(hipMemcpyAsync(ctx->w_msg.p, base + lo, span, hipMemcpyHostToDevice, st), "H2D data");
-    NW_TRY(hipMemcpyAsync(ctx->w_msg_off.p, roff.data(), n * 8, hipMemcpyHostToDevice, st), "H2D off");
-    NW_TRY(hipMemcpyAsync(ctx->w_msg_len.p, len, n * 8, hipMemcpyHostToDevice, st), "H2D len");
-    NW_TRY(launch_sha512_many((uint32_t)n, ctx->w_msg.as<uint8_t>(), ctx->w_msg_off.as<uint64_t>(),
-                              ctx->w_msg_len.as<uint64_t>(), ctx->w_out.as<uint8_t>(), st),
+    Lease lease(ctx);
+    Workspace* ws = lease.ws();
+    if (!ws) return NW_ERR_DEVICE;
+    hipStream_t st = ws->stream;
+    NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
+    NW_TRY(ws->ensure(ws->w_msg, span + 16), "ws msg");
+    NW_TRY(ws->ensure(ws->w_msg_off, n * 8), "ws off");
+    NW_TRY(ws->ensure(ws->w_msg_len, n * 8), "ws len");
+    NW_TRY(ws->ensure(ws->w_out, n * 64), "ws out");
+    if (span) NW_TRY(hipMemcpyAsync(ws->w_msg.p, base + lo, span, hipMemcpyHostToDevice, st), "H2D data");
+    NW_TRY(hipMemcpyAsync(ws->w_msg_off.p, roff.data(), n * 8, hipMemcpyHostToDevice, st), "H2D off");
+    NW_TRY(hipMemcpyAsync(ws->w_msg_len.p, len, n * 8, hipMemcpyHostToDevice, st), "H2D len");
+    NW_TRY(launch_sha512_many((uint32_t)n, ws->w_msg.as<uint8_t>(), ws->w_msg_off.as<uint64_t>(),
+                              ws->w_msg_len.as<uint64_t>(), ws->w_out.as<uint8_t>(), st),
            "k_sha512_many");
-    NW_TRY(hipMemcpyAsync(out, ctx->w_out.p, n * 64, hipMemcpyDeviceToHost, st), "D2H digests");
+    NW_TRY(hipMemcpyAsync(out, ws->w_out.p, n * 64, hipMemcpyDeviceToHost, st), "D2H digests");
     NW_TRY(hipStreamSynchronize(st), "sync");
+    lease.synced();
     return NW_OK;
 }
 
@@ -762,8 +1206,9 @@ int nw_sha512(nw_ctx* ctx, const uint8_t* data, size_t len, uint8_t out[64]) {
 int nw_sign_many_dev(nw_ctx* ctx, const uint8_t* d_seed32, const uint8_t* d_msgs, size_t msg_len, size_t n,
                      uint8_t* d_pk32, uint8_t* d_sig64, void* stream) {
     if (!ctx || (msg_len != 8 && msg_len != 32)) return NW_ERR_ARG;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n > 0xFFFFFFF0u || (n && (!d_seed32 || !d_msgs))) return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);   // reads the basepoint table
     NW_TRY(launch_sign((uint32_t)n, (int)(msg_len / 4), reinterpret_cast<const uint32_t*>(d_seed32),
                        reinterpret_cast<const uint32_t*>(d_msgs), ctx->d_btab, reinterpret_cast<uint32_t*>(d_pk32),
                        reinterpret_cast<uint32_t*>(d_sig64), reinterpret_cast<hipStream_t>(stream)),
@@ -775,14 +1220,18 @@ int nw_sign_many(nw_ctx* ctx, const uint8_t (*seed)[32], const uint8_t* msgs, si
                  uint8_t (*pk)[32], uint8_t (*sig)[64]) {
     if (!ctx || (msg_len != 8 && msg_len != 32) || (n && (!seed || !msgs))) return NW_ERR_ARG;
     if (n == 0) return NW_OK;
-    std::lock_guard<std::mutex> g(ctx->mu);
+    if (n > 0xFFFFFFF0u) return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
-    hipStream_t st = ctx->stream;
-    NW_TRY(ctx->w_misc.ensure(n * 32 + n * msg_len + 16), "ws misc");
-    NW_TRY(ctx->w_out.ensure(n * 96 + 16), "ws out");
-    uint8_t* d_seed = ctx->w_misc.as<uint8_t>();
+    Lease lease(ctx);
+    Workspace* ws = lease.ws();
+    if (!ws) return NW_ERR_DEVICE;
+    hipStream_t st = ws->stream;
+    NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
+    NW_TRY(ws->ensure(ws->w_misc, n * 32 + n * msg_len + 16), "ws misc");
+    NW_TRY(ws->ensure(ws->w_out, n * 96 + 16), "ws out");
+    uint8_t* d_seed = ws->w_misc.as<uint8_t>();
     uint8_t* d_msg = d_seed + n * 32;
-    uint8_t* d_pk = ctx->w_out.as<uint8_t>();
+    uint8_t* d_pk = ws->w_out.as<uint8_t>();
     uint8_t* d_sig = d_pk + n * 32;
     NW_TRY(hipMemcpyAsync(d_seed, seed, n * 32, hipMemcpyHostToDevice, st), "H2D seed");
     NW_TRY(hipMemcpyAsync(d_msg, msgs, n * msg_len, hipMemcpyHostToDevice, st), "H2D msg");
@@ -793,6 +1242,7 @@ int nw_sign_many(nw_ctx* ctx, const uint8_t (*seed)[32], const uint8_t* msgs, si
     if (pk) NW_TRY(hipMemcpyAsync(pk, d_pk, n * 32, hipMemcpyDeviceToHost, st), "D2H pk");
     if (sig) NW_TRY(hipMemcpyAsync(sig, d_sig, n * 64, hipMemcpyDeviceToHost, st), "D2H sig");
     NW_TRY(hipStreamSynchronize(st), "sync");
+    lease.synced();
     return NW_OK;
 }
 

@@ -47,10 +47,13 @@ struct VerifyParams {
     uint32_t* pbuf;                // [PREC_ROWS][n] SoA, processing order: P's X, Z + partial flags
     uint32_t* pre;                 // [10][n] SoA prefix products of Z (k_finish scratch)
     const uint32_t* perm;          // [n] processing order for k_verify (signer-grouped) or null
+    uint32_t nkeys;                // key-cache slots (signer slots >= nkeys are rejected, never read)
+    const uint32_t* sig_keys;      // k_verify_var: [n][8] raw key words of each signature (uncached keys)
 };
 
 struct FinalizeParams {
     uint32_t ncerts;
+    uint32_t nsigs;                // vote ranges past nsigs reject their certificate
     const uint32_t* cert_first;
     const uint32_t* cert_n;
     const uint32_t* flags;
@@ -69,8 +72,10 @@ hipError_t launch_group_by_signer(uint32_t n, uint32_t nkeys, const uint32_t* si
 hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st);
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st);
 // Also zeroes zero4[0..3] (the slow-path counter) when ncerts > 0, saving a memset launch.
-hipError_t launch_expand_certs(uint32_t ncerts, const uint32_t* first, const uint32_t* nv, uint32_t* sig_cert,
-                               uint32_t* zero4, hipStream_t st);
+hipError_t launch_expand_certs(uint32_t ncerts, uint32_t nsigs, const uint32_t* first, const uint32_t* nv,
+                               uint32_t* sig_cert, uint32_t* zero4, hipStream_t st);
+hipError_t launch_validate_certs(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
+                                 const uint32_t* nv, const uint32_t* signer, uint32_t* status, hipStream_t st);
 hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hipStream_t st);
 hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
                            uint32_t* tab, int window, hipStream_t st);

@@ -41,9 +41,13 @@ extern template hipError_t launch_vs_wa<20>(const VerifyParams&, int, bool, uint
 static constexpr uint32_t GROUP_TILE = 4096;
 static constexpr uint32_t GROUP_LDS_KEYS = 8192;
 
-__global__ void __launch_bounds__(256) k_count_slots(uint32_t n, const uint32_t* signer, uint32_t* counts) {
+// Out-of-range slots (rejected by k_verify) are grouped with slot 0 so no access leaves the arrays.
+__device__ __forceinline__ uint32_t clamp_slot(uint32_t s, uint32_t nkeys) { return s < nkeys ? s : 0u; }
+
+__global__ void __launch_bounds__(256) k_count_slots(uint32_t n, uint32_t nkeys, const uint32_t* signer,
+                                                     uint32_t* counts) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(&counts[signer[i]], 1u);
+    if (i < n) atomicAdd(&counts[clamp_slot(signer[i], nkeys)], 1u);
 }
 
 __global__ void __launch_bounds__(256) k_count_slots_lds(uint32_t n, uint32_t nkeys, const uint32_t* signer,
@@ -53,7 +57,7 @@ __global__ void __launch_bounds__(256) k_count_slots_lds(uint32_t n, uint32_t nk
     __syncthreads();
     const uint32_t t0 = blockIdx.x * GROUP_TILE;
     const uint32_t t1 = min(n, t0 + GROUP_TILE);
-    for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&hist[signer[i]], 1u);
+    for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&hist[clamp_slot(signer[i], nkeys)], 1u);
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < nkeys; k += blockDim.x)
         if (hist[k]) atomicAdd(&counts[k], hist[k]);
@@ -83,10 +87,10 @@ __global__ void __launch_bounds__(1024) k_scan_slots(uint32_t k, const uint32_t*
     }
 }
 
-__global__ void __launch_bounds__(256) k_scatter_slots(uint32_t n, const uint32_t* signer, uint32_t* cursor,
-                                                       uint32_t* perm) {
+__global__ void __launch_bounds__(256) k_scatter_slots(uint32_t n, uint32_t nkeys, const uint32_t* signer,
+                                                       uint32_t* cursor, uint32_t* perm) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) perm[atomicAdd(&cursor[signer[i]], 1u)] = i;
+    if (i < n) perm[atomicAdd(&cursor[clamp_slot(signer[i], nkeys)], 1u)] = i;
 }
 
 // Tile-local scatter: LDS histogram -> one global atomic per (tile, slot) reserves the tile's run
@@ -103,13 +107,13 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
     __syncthreads();
     const uint32_t t0 = blockIdx.x * GROUP_TILE;
     const uint32_t t1 = min(n, t0 + GROUP_TILE);
-    for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&base[signer[i]], 1u);
+    for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&base[clamp_slot(signer[i], nkeys)], 1u);
     __syncthreads();
     for (uint32_t k = threadIdx.x; k < nkeys; k += blockDim.x)
         if (base[k]) base[k] = atomicAdd(&cursor[k], base[k]);
     __syncthreads();
     for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
-        const uint32_t k = signer[i];
+        const uint32_t k = clamp_slot(signer[i], nkeys);
         perm[base[k] + atomicAdd(&rank[k], 1u)] = i;
     }
 }
@@ -170,8 +174,12 @@ __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (c >= a.ncerts) return;   // whole wave exits together
-    const uint32_t first = a.cert_first[c], nv = a.cert_n[c];
-    bool bad = false, slow = false;
+    const uint32_t first = a.cert_first[c];
+    // a vote range past the signature array (device inputs are not host-checked) rejects the
+    // certificate; only the in-range votes are read
+    const bool range_bad = (uint64_t)first + a.cert_n[c] > a.nsigs;
+    const uint32_t nv = range_bad ? (first < a.nsigs ? a.nsigs - first : 0u) : a.cert_n[c];
+    bool bad = range_bad, slow = false;
     uint32_t tsum = 0;
     uint64_t stake = 0;
     for (uint32_t v = lane; v < nv; v += 64) {
@@ -211,13 +219,27 @@ __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
     if (a.accepted_stake) a.accepted_stake[c] = stake;
 }
 
-__global__ void __launch_bounds__(256) k_expand_certs(uint32_t ncerts, const uint32_t* cert_first,
+__global__ void __launch_bounds__(256) k_expand_certs(uint32_t ncerts, uint32_t nsigs, const uint32_t* cert_first,
                                                       const uint32_t* cert_n, uint32_t* sig_cert, uint32_t* zero4) {
     const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c < 4) zero4[c] = 0u;   // ncerts >= 1: the launch has at least 256 threads
     if (c >= ncerts) return;
     const uint32_t f = cert_first[c], n = cert_n[c];
-    for (uint32_t v = 0; v < n; ++v) sig_cert[f + v] = c;
+    const uint32_t end = (uint64_t)f + n > nsigs ? nsigs : f + n;   // clamped: k_cert_finalize rejects
+    for (uint32_t v = f; v < end; ++v) sig_cert[v] = c;
+}
+
+// Device-side input check of nw_verify_certs_dev: every vote range inside [0, nsigs) and every
+// signer slot inside the key cache; *status |= NW_ERR_ARG otherwise (the verify kernels clamp the
+// same inputs, so a bad call never reads outside its arrays).
+__global__ void __launch_bounds__(256) k_validate_certs(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys,
+                                                        const uint32_t* cert_first, const uint32_t* cert_n,
+                                                        const uint32_t* signer, uint32_t* status) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    bool bad = false;
+    if (t < ncerts) bad = (uint64_t)cert_first[t] + cert_n[t] > nsigs;
+    if (t < nsigs) bad = bad || signer[t] >= nkeys;
+    if (bad) atomicOr(status, (uint32_t)NW_ERR_ARG);
 }
 
 __global__ void __launch_bounds__(256) k_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok) {
@@ -330,13 +352,14 @@ hipError_t launch_group_by_signer(uint32_t n, uint32_t nkeys, const uint32_t* si
         hipLaunchKernelGGL(k_count_slots_lds, dim3(blocks_for(n, GROUP_TILE)), dim3(256), nkeys * 4, st, n, nkeys,
                            signer, counts);
     else
-        hipLaunchKernelGGL(k_count_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, signer, counts);
+        hipLaunchKernelGGL(k_count_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, nkeys, signer, counts);
     hipLaunchKernelGGL(k_scan_slots, dim3(1), dim3(1024), 0, st, nkeys, counts, cursor);
     if (lds)
         hipLaunchKernelGGL(k_scatter_slots_lds, dim3(blocks_for(n, GROUP_TILE)), dim3(256), nkeys * 8, st, n, nkeys,
                            signer, cursor, perm);
     else
-        hipLaunchKernelGGL(k_scatter_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, signer, cursor, perm);
+        hipLaunchKernelGGL(k_scatter_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, nkeys, signer, cursor,
+                           perm);
     return hipGetLastError();
 }
 
@@ -354,11 +377,20 @@ hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_expand_certs(uint32_t ncerts, const uint32_t* first, const uint32_t* nv, uint32_t* sig_cert,
-                               uint32_t* zero4, hipStream_t st) {
+hipError_t launch_expand_certs(uint32_t ncerts, uint32_t nsigs, const uint32_t* first, const uint32_t* nv,
+                               uint32_t* sig_cert, uint32_t* zero4, hipStream_t st) {
     if (ncerts == 0) return hipMemsetAsync(zero4, 0, 16, st);
-    hipLaunchKernelGGL(k_expand_certs, dim3(blocks_for(ncerts, 256)), dim3(256), 0, st, ncerts, first, nv,
+    hipLaunchKernelGGL(k_expand_certs, dim3(blocks_for(ncerts, 256)), dim3(256), 0, st, ncerts, nsigs, first, nv,
                        sig_cert, zero4);
+    return hipGetLastError();
+}
+
+hipError_t launch_validate_certs(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
+                                 const uint32_t* nv, const uint32_t* signer, uint32_t* status, hipStream_t st) {
+    const uint32_t n = ncerts > nsigs ? ncerts : nsigs;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_validate_certs, dim3(blocks_for(n, 256)), dim3(256), 0, st, ncerts, nsigs, nkeys, first, nv,
+                       signer, status);
     return hipGetLastError();
 }
 

@@ -381,6 +381,12 @@ int nw_cert_batch_verify(nw_ctx* ctx, const nw_cert_batch* b, const uint8_t zsee
     std::vector<uint8_t> dig(off.size() * 64);
     int rc = nw_sha512_many(ctx, buf.data(), off.data(), len.data(), off.size(), reinterpret_cast<uint8_t(*)[64]>(dig.data()));
     if (rc != NW_OK) return rc;
+    // Committee keys go to the context's key cache once (nw_committee_load deduplicates), so the
+    // header signatures and the vote batches below take the cached comb path.
+    std::vector<uint32_t> slot(b->names.size());
+    rc = nw_committee_load(ctx, reinterpret_cast<const uint8_t(*)[32]>(b->names.data()), b->stakes.data(),
+                           b->names.size(), slot.data());
+    if (rc != NW_OK) return rc;
     // 2. Header::verify: id, then the host checks, then the strict signature (one submission)
     std::vector<size_t> live;
     for (size_t k = 0; k < todo.size(); ++k) {
@@ -414,12 +420,7 @@ int nw_cert_batch_verify(nw_ctx* ctx, const nw_cert_batch* b, const uint8_t zsee
         live.swap(nxt);
     }
     if (live.empty()) return NW_OK;
-    // 3. Signature::verify_batch of every remaining certificate: one submission.  Committee keys
-    //    go to the context's key cache once (nw_committee_load deduplicates).
-    std::vector<uint32_t> slot(b->names.size());
-    rc = nw_committee_load(ctx, reinterpret_cast<const uint8_t(*)[32]>(b->names.data()), b->stakes.data(),
-                           b->names.size(), slot.data());
-    if (rc != NW_OK) return rc;
+    // 3. Signature::verify_batch of every remaining certificate: one submission.
     std::vector<nw_cert> certs;
     std::vector<uint32_t> signer;
     std::vector<uint8_t> sigs, msgs;

@@ -19,8 +19,10 @@ __device__ __forceinline__ void lane_inputs(const VerifyParams& a, uint32_t i, u
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
     load_w8(S, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16 + 8);
     slot = a.signer[i];
+    const bool in_cache = slot < a.nkeys;   // device inputs: an out-of-range slot is rejected
+    slot = in_cache ? slot : 0u;
     load_w8(Aw, a.keys_raw + (size_t)slot * 8);
-    kinfo = a.key_info[slot];
+    kinfo = in_cache ? a.key_info[slot] : 0u;
     cert = a.sig_cert[i];
     if (MSGMODE == 0) {
         uint32_t M[8];

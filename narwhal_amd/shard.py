@@ -79,10 +79,10 @@ def allgather_verdicts(ok_local, stake_local, ranges: List[Tuple[int, int]], gro
     return torch.cat(oks), torch.cat(stakes)
 
 
-def verify_sharded(engine, cs, slots, zseed: bytes, rank: int, world: int, group=None):
+def verify_sharded(engine, cs, slots, zseed: bytes, rank: int, world: int, group=None, device=None):
     """Verify this rank's shard of ``cs`` (narwhal_amd.workload.Certificates) on its GPU and
     all-gather the node-wide verdicts.  Returns (cert_ok uint8[C], stake int64[C]) torch tensors on
-    this rank's device."""
+    ``device`` (default: this rank's GPU)."""
     import torch
     ranges = partition(cs.cert_n, world)
     c0, c1 = ranges[rank]
@@ -90,6 +90,37 @@ def verify_sharded(engine, cs, slots, zseed: bytes, rank: int, world: int, group
     f1 = int(cs.cert_first[c1 - 1] + cs.cert_n[c1 - 1]) if c1 > c0 else 0
     ok, _, st = engine.verify_certs_np(cs.cert_first[c0:c1] - f0, cs.cert_n[c0:c1], cs.sigs[f0:f1],
                                        slots[cs.signer[f0:f1]], cs.msgs[c0:c1], zseed, cert_base=c0)
-    dev = torch.device("cuda", torch.cuda.current_device())
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     return allgather_verdicts(torch.from_numpy(ok).to(dev), torch.from_numpy(st.astype(np.int64)).to(dev), ranges,
                               group)
+
+
+def split_bounds(n: int, world: int) -> List[Tuple[int, int]]:
+    """Contiguous vote ranges of one batch split over ``world`` ranks."""
+    return [((n * r) // world, (n * (r + 1)) // world) for r in range(world)]
+
+
+def verify_split_batch(engine, msgs, pks, sigs, zseed: bytes, batch_index: int, rank: int, world: int,
+                       group=None, device=None) -> bool:
+    """One huge batch (e.g. a 6,667-vote certificate at N = 10,000) split across the ranks
+    (SURVEY.md §8(e)): each rank evaluates its votes' share of dalek's batch equation
+    (nw_verify_batch_partial; coefficients keyed by the vote's index in the whole batch, so no
+    transcript exchange is needed), ONE all-gather exchanges the 160-byte partial points and the
+    parse/decode flags, and every rank tests the sum for the identity.  The group arithmetic is
+    exact, so the verdict equals the unsplit nw_verify_batch verdict."""
+    import torch
+    import torch.distributed as dist
+    from ._lib import POINT_BYTES
+    a, b = split_bounds(len(sigs), world)[rank]
+    pt, bad = engine.verify_batch_partial(msgs[a:b], pks[a:b], sigs[a:b], zseed, batch_index, a)
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    buf = torch.zeros(POINT_BYTES + 8, dtype=torch.uint8)
+    buf[:POINT_BYTES] = torch.frombuffer(bytearray(pt), dtype=torch.uint8)
+    buf[POINT_BYTES] = 1 if bad else 0
+    buf = buf.to(dev)
+    gathered = [torch.empty_like(buf) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(gathered, buf, group=group)
+    rows = [g.cpu().numpy() for g in gathered]
+    if any(int(r[POINT_BYTES]) for r in rows):
+        return False
+    return engine.points_sum_is_identity([bytes(r[:POINT_BYTES]) for r in rows])

@@ -13,6 +13,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the built libnwcrypto.so")
 
 
+@pytest.fixture(scope="session", autouse=True)
+def _torch_gpu_first(request):
+    """GPU sessions: let torch (which bundles its own HIP runtime) initialise the device before
+    libnwcrypto's runtime does; in the other order torch reports "No HIP GPUs are available".
+    bench.py does the same (torch.cuda.set_device before the first Engine)."""
+    if any(item.get_closest_marker("gpu") is not None for item in request.session.items):
+        import torch
+        torch.cuda.set_device(0)
+        torch.zeros(1, device="cuda:0")
+    yield
+
+
 @pytest.fixture(scope="session")
 def golden():
     import json

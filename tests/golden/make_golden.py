@@ -170,8 +170,11 @@ def main():
         assert want
         batches.append({"name": "cancelling_pair", "zseed": h(zseed), "batch_index": bidx,
                         "items": [[h(k), h(s), h(m)] for k, s, m in items], "ok": True})
+        # the same items under the coefficients of another batch index: computed, not assumed
+        zs2 = o.batch_coefficients(zseed, bidx + 100, len(items))
+        want2 = o.verify_batch_z([m for _, _, m in items], [s for _, s, _ in items], [k for k, _, _ in items], zs2)
         batches.append({"name": "cancelling_pair_other_z", "zseed": h(zseed), "batch_index": bidx + 100,
-                        "items": [[h(k), h(s), h(m)] for k, s, m in items], "ok": False})
+                        "items": [[h(k), h(s), h(m)] for k, s, m in items], "ok": want2})
     out["adversarial_batch"] = batches
 
     # ---------------------------------------------------------------- coefficient stream pin

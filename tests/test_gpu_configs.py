@@ -1,0 +1,219 @@
+"""GPU parity at every BASELINE.json config, on the committee-mode engine the
+bench and the Rust shim use (key_window = -1: W20 at 100 keys, W16 at 1,000, W12 at 10,000).
+
+  C2  100 validators, 14,926 certificates x 67 votes (1,000,042 sigs): the benchmarked W20 kernel
+  C3  1,000 validators, one round of 1,000 certificates x 667 votes: every certificate vs the oracle
+  C5  C3 with 1% adversarial signatures (tests/adversarial_mix.py): every certificate verdict and
+      every adversarial strict verdict vs the oracle
+  C4  10,000 validators, one GPU's share of a round (1,250 certificates x 6,667 votes, W12)
+  W   worker batch digests (worker/src/processor.rs:65): 508,052-B and 1,000,012-B batches
+
+The checker is oracle/nw_ref.c (C restatement of dalek 1.0.1's verify_batch / verify_strict),
+pinned against the Python oracle and the golden vectors by the CPU tests.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import nw_ref
+
+pytestmark = pytest.mark.gpu
+
+ZSEED = bytes(range(32))
+THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def _engine(window=-1):
+    from narwhal_amd import _lib
+    return _lib.Engine(device=0, key_window=window)
+
+
+def _setup(eng, validators, ncerts, votes):
+    from narwhal_amd import workload
+    com = workload.make_committee(validators, eng)
+    slots = eng.committee_load_np(com.pks, com.stake)
+    cs = workload.make_certificates(com, ncerts, votes, eng)
+    return com, slots, cs
+
+
+def _verify(eng, cs, slots, zseed=ZSEED, cert_base=0):
+    return eng.verify_certs_np(cs.cert_first, cs.cert_n, cs.sigs, slots[cs.signer], cs.msgs, zseed, cert_base)
+
+
+# ----------------------------------------------------------------------------- C2 at W20
+# Class-scoped engines: each holds up to ~100 GB of key tables, so one config's engine is closed
+# before the next one is built.
+@pytest.fixture(scope="class")
+def c2():
+    eng = _engine()
+    com, slots, cs = _setup(eng, 100, 14926, 67)
+    yield eng, com, slots, cs
+    eng.close()
+
+
+class TestC2W20:
+    def test_c2_committee_mode_is_w20(self, c2):
+        eng, com, slots, cs = c2
+        assert eng.key_window() == 20 and eng.committee_size() == 100
+        assert cs.nsigs == 1000042
+
+    def test_c2_w20_all_valid(self, c2):
+        eng, com, slots, cs = c2
+        cert_ok, sig_ok, stake = _verify(eng, cs, slots, os.urandom(32))
+        assert cert_ok.all() and sig_ok.all() and (stake == 67).all()
+        sel = list(range(0, cs.ncerts, 149))
+        assert all(nw_ref.verify_certs(cs, com, sel, ZSEED, THREADS))
+
+    def test_c2_w20_corruptions_vs_oracle(self, c2):
+        """Exactly the certificates holding a corrupted vote fail; the per-signature bitmap flags
+        exactly the corrupted votes; every failing certificate and 100 passing ones agree with the
+        oracle's batch equation under the same coefficients."""
+        eng, com, slots, cs0 = c2
+        import copy
+        cs = copy.copy(cs0)
+        rng = np.random.default_rng(3)
+        cs.sigs = cs0.sigs.copy()
+        bad = rng.choice(cs.nsigs, 300, replace=False)
+        kind = rng.integers(0, 3, size=bad.shape[0])
+        for b, k in zip(bad, kind):
+            if k == 0:
+                cs.sigs[b, 40] ^= 1
+            elif k == 1:
+                cs.sigs[b, 3] ^= 0x10
+            else:
+                cs.sigs[b, 63] |= 0xE0
+        cert_ok, sig_ok, stake = _verify(eng, cs, slots)
+        exp_sig = np.ones(cs.nsigs, bool)
+        exp_sig[bad] = False
+        assert (sig_ok.astype(bool) == exp_sig).all()
+        bad_certs = sorted(set((bad // 67).tolist()))
+        exp_cert = np.ones(cs.ncerts, bool)
+        exp_cert[bad_certs] = False
+        assert (cert_ok.astype(bool) == exp_cert).all()
+        good = [c for c in range(0, cs.ncerts, 97) if exp_cert[c]][:100]
+        sel = bad_certs + good
+        want = nw_ref.verify_certs(cs, com, sel, ZSEED, THREADS)
+        assert [bool(cert_ok[c]) for c in sel] == want
+        assert [int(stake[c]) for c in bad_certs] == [67 - int((bad // 67 == c).sum()) for c in bad_certs]
+
+    def test_c2_w20_device_path_matches_host_path(self, c2):
+        """nw_verify_certs_dev (the benchmarked entry point) on HBM-resident inputs, asynchronous
+        status word: same verdicts and flags as the host-buffer path."""
+        import torch
+        eng, com, slots, cs = c2
+        dev = torch.device("cuda", 0)
+        sigs = cs.sigs.copy()
+        sigs[5, 40] ^= 1
+        d_sig = torch.from_numpy(sigs).to(dev)
+        d_signer = torch.from_numpy(slots[cs.signer].astype(np.int32)).to(dev)
+        d_first = torch.from_numpy(cs.cert_first.astype(np.int32)).to(dev)
+        d_n = torch.from_numpy(cs.cert_n.astype(np.int32)).to(dev)
+        d_msg = torch.from_numpy(cs.msgs).to(dev)
+        d_ok = torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev)
+        d_flags = torch.zeros(cs.nsigs, dtype=torch.int32, device=dev)
+        d_stake = torch.zeros(cs.ncerts, dtype=torch.int64, device=dev)
+        d_status = torch.full((1,), 77, dtype=torch.int32, device=dev)
+        st = torch.cuda.current_stream()
+        eng.verify_certs_dev(cs.ncerts, d_first.data_ptr(), d_n.data_ptr(), cs.nsigs, d_sig.data_ptr(),
+                             d_signer.data_ptr(), d_msg.data_ptr(), ZSEED, 0, d_ok.data_ptr(), d_flags.data_ptr(),
+                             d_stake.data_ptr(), st.cuda_stream, d_status=d_status.data_ptr())
+        torch.cuda.synchronize()
+        assert int(d_status.item()) == 0
+        import copy
+        cs2 = copy.copy(cs)
+        cs2.sigs = sigs
+        cert_ok, sig_ok, stake = _verify(eng, cs2, slots)
+        assert (d_ok.cpu().numpy() == cert_ok).all()
+        assert ((d_flags.cpu().numpy() & 0x8 != 0) == sig_ok.astype(bool)).all()
+        assert (d_stake.cpu().numpy() == stake.astype(np.int64)).all()
+        assert not cert_ok[0] and cert_ok[1:].all()
+
+
+# ----------------------------------------------------------------------------- C3 / C5
+@pytest.fixture(scope="class")
+def c3():
+    eng = _engine()
+    com, slots, cs = _setup(eng, 1000, 1000, 667)
+    yield eng, com, slots, cs
+    eng.close()
+
+
+class TestC3C5:
+    def test_c3_every_certificate_vs_oracle(self, c3):
+        eng, com, slots, cs = c3
+        assert eng.key_window() == 16 and cs.nsigs == 667000
+        cert_ok, sig_ok, stake = _verify(eng, cs, slots)
+        want = nw_ref.verify_certs(cs, com, list(range(cs.ncerts)), ZSEED, THREADS)
+        assert cert_ok.astype(bool).tolist() == want
+        assert all(want) and sig_ok.all() and (stake == 667).all()
+
+    def test_c5_adversarial_mix_vs_oracle(self, c3):
+        """1% of the C3 signatures replaced by classes (ii)/(iii)/(v)/(vi)/(vii)/(viii)/(ix): every
+        certificate's batch verdict and every adversarial signature's strict verdict match the oracle
+        (nearly every certificate takes the per-signature fallback)."""
+        import copy
+        from adversarial_mix import make_adversarial
+        eng, com, slots, cs0 = c3
+        cs = copy.copy(cs0)
+        kinds = make_adversarial(cs, com, 0.01, np.random.default_rng(5))
+        assert len(kinds) == 6670
+        for base in (0, 7000):   # two coefficient streams: the torsion classes depend on z
+            cert_ok, sig_ok, stake = _verify(eng, cs, slots, ZSEED, base)
+            want = nw_ref.verify_certs(cs, com, list(range(cs.ncerts)), ZSEED, THREADS, cert_base=base)
+            got = cert_ok.astype(bool).tolist()
+            assert got == want, [c for c in range(cs.ncerts) if got[c] != want[c]][:10]
+        cert_of = np.repeat(np.arange(cs.ncerts), cs.cert_n.astype(np.int64))
+        bad = []
+        for i, cls in kinds.items():
+            w = nw_ref.verify_strict(bytes(com.pks[cs.signer[i]]), bytes(cs.msgs[cert_of[i]]), bytes(cs.sigs[i]))
+            if bool(sig_ok[i]) != w:
+                bad.append((i, cls))
+        assert not bad, bad[:10]
+        honest = np.ones(cs.nsigs, bool)
+        honest[list(kinds)] = False
+        assert sig_ok[honest].all()
+        # accepted stake counts exactly the strictly valid votes
+        exp_stake = np.bincount(cert_of, weights=sig_ok.astype(np.int64), minlength=cs.ncerts)
+        assert (stake == exp_stake).all()
+
+
+# ----------------------------------------------------------------------------- C4
+def test_c4_w12_sample_vs_oracle_and_localized():
+    eng = _engine()
+    try:
+        com, slots, cs = _setup(eng, 10000, 1250, 6667)
+        assert eng.key_window() == 12 and cs.nsigs == 1250 * 6667
+        rng = np.random.default_rng(9)
+        bad = rng.choice(cs.nsigs, 40, replace=False)
+        sigs = cs.sigs
+        orig = sigs[bad].copy()
+        sigs[bad, 40] ^= 1
+        cert_ok, sig_ok, stake = _verify(eng, cs, slots)
+        exp_sig = np.ones(cs.nsigs, bool)
+        exp_sig[bad] = False
+        assert (sig_ok.astype(bool) == exp_sig).all()
+        bad_certs = sorted(set((bad // 6667).tolist()))
+        exp_cert = np.ones(cs.ncerts, bool)
+        exp_cert[bad_certs] = False
+        assert (cert_ok.astype(bool) == exp_cert).all()
+        sel = bad_certs[:8] + [c for c in range(0, cs.ncerts, 150) if exp_cert[c]][:8]
+        assert [bool(cert_ok[c]) for c in sel] == nw_ref.verify_certs(cs, com, sel, ZSEED, THREADS)
+        sigs[bad] = orig
+    finally:
+        eng.close()
+
+
+# ----------------------------------------------------------------------------- worker digests
+@pytest.mark.parametrize("n_tx,tx_size", [(977, 512), (62500, 8)])
+def test_worker_batch_digests_vs_hashlib(engine, n_tx, tx_size):
+    """SHA512(bincode WorkerMessage::Batch) of 508,052-B (512-B tx) and 1,000,012-B (8-B tx)
+    batches, 16 of each at once, plus one lone batch."""
+    from narwhal_amd import workload
+    host = workload.worker_batches_np(16, n_tx, tx_size)
+    assert host.shape[1] == 12 + n_tx * (8 + tx_size)
+    assert bytes(host[3]) == workload.worker_batch(n_tx, tx_size, 3)
+    got = engine.sha512_many([bytes(b) for b in host])
+    assert got == [hashlib.sha512(bytes(b)).digest() for b in host]
+    assert engine.sha512(bytes(host[0])) == hashlib.sha512(bytes(host[0])).digest()

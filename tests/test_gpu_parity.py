@@ -282,27 +282,6 @@ def test_c2_corruptions_localized(engine, c2):
         assert o.crypto_verify_batch(bytes(cs.msgs[c]), votes, bytes(32), c) == bool(cert_ok[c])
 
 
-# ----------------------------------------------------------------------------- key-window variants
-@pytest.mark.parametrize("window", [8, 12])
-def test_key_windows_adversarial(window, golden):
-    """The committee comb window (8 / 12 / 16 bits, chosen by committee size) never changes a verdict."""
-    from narwhal_amd import _lib
-    eng = _lib.Engine(device=0, key_window=window)
-    cases = golden["adversarial_strict"]
-    got = eng.verify_strict_many([bytes.fromhex(c["msg"]) for c in cases], [bytes.fromhex(c["pk"]) for c in cases],
-                                 [bytes.fromhex(c["sig"]) for c in cases])
-    assert [c["name"] for c, g in zip(cases, got) if g != c["strict"]] == []
-    bad = []
-    for c in golden["adversarial_batch"][::3]:
-        items = [(bytes.fromhex(k), bytes.fromhex(s), bytes.fromhex(m)) for k, s, m in c["items"]]
-        got = eng.verify_batch([m for *_, m in items], [k for k, _, _ in items], [s for _, s, _ in items],
-                               bytes.fromhex(c["zseed"]), c["batch_index"])
-        if got != c["ok"]:
-            bad.append(c["name"])
-    assert not bad
-    eng.close()
-
-
 # ----------------------------------------------------------------------------- worker load (A13)
 def test_verify_batches_worker_chunks(engine):
     """worker/src/processor.rs:75-79: fixed keypairs, 8-byte LE messages i, the batch split into

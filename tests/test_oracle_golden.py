@@ -79,14 +79,17 @@ def test_adversarial_strict_oracle(golden):
         assert got == c["strict"], c["name"]
 
 
-def test_adversarial_batch_oracle_sample(golden):
-    """Re-derive a sample of the batch verdicts (the full set is regenerated by make_golden.py)."""
-    for c in golden["adversarial_batch"][::9]:
+def test_adversarial_batch_oracle_all(golden):
+    """Re-derive every golden batch verdict on the oracle (196 batches, ~5 s), including the
+    computed ``cancelling_pair_other_z`` cases."""
+    names = {c["name"] for c in golden["adversarial_batch"]}
+    assert "cancelling_pair_other_z" in names and "cancelling_pair" in names
+    for c in golden["adversarial_batch"]:
         items = [(bytes.fromhex(k), bytes.fromhex(s), bytes.fromhex(m)) for k, s, m in c["items"]]
         pre = all(s[63] & 0xE0 == 0 and o.decompress(k) is not None for k, s, _ in items)
         zs = o.batch_coefficients(bytes.fromhex(c["zseed"]), c["batch_index"], len(items))
         got = pre and o.verify_batch_z([m for *_, m in items], [s for _, s, _ in items], [k for k, _, _ in items], zs)
-        assert got == c["ok"], c["name"]
+        assert got == c["ok"], (c["name"], c["batch_index"])
 
 
 def test_torsion_semantics_known_cases():

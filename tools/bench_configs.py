@@ -46,11 +46,13 @@ def time_gpu(eng, cs, slots, zseed, steps, warmup, cert_base=0):
     d_ok = torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev)
     d_flags = torch.zeros(cs.nsigs, dtype=torch.int32, device=dev)
     d_stake = torch.zeros(cs.ncerts, dtype=torch.int64, device=dev)
+    d_status = torch.zeros(1, dtype=torch.int32, device=dev)
 
     def step():
         eng.verify_certs_dev(cs.ncerts, d_first.data_ptr(), d_n.data_ptr(), cs.nsigs, d_sig.data_ptr(),
                              d_signer.data_ptr(), d_msg.data_ptr(), zseed, cert_base, d_ok.data_ptr(),
-                             d_flags.data_ptr(), d_stake.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                             d_flags.data_ptr(), d_stake.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                             d_status=d_status.data_ptr())
 
     for _ in range(warmup):
         step()
