@@ -3,6 +3,10 @@
 The shared library is built in-tree (``narwhal_amd/libnwcrypto.so``, see ``__graft_entry__.build``).
 There is deliberately no CPU fallback: a missing library raises ``ImportError`` here, and a
 missing/unusable GPU makes every context creation fail with ``DeviceError``.
+
+Processes that also use PyTorch must ``import torch`` BEFORE importing this module: torch bundles
+its own HIP runtime with the same soname (libamdhip64.so.7), the first one loaded serves both, and
+only the torch-first order gives both of them the GPU (tools/probe_runtime.sh on the MI355X box).
 """
 from __future__ import annotations
 

@@ -3,6 +3,15 @@ import sys
 
 import pytest
 
+# torch ships its own HIP runtime under the same soname (libamdhip64.so.7) as the /opt/rocm one
+# libnwcrypto.so links.  Whichever library is loaded FIRST provides the runtime for both; with
+# libnwcrypto's loaded first torch reports "No HIP GPUs are available" (measured on the MI355X box,
+# tools/probe_runtime.sh), so torch is imported before anything loads the library.
+try:
+    import torch  # noqa: F401
+except ImportError:   # pragma: no cover - torch is part of the image
+    torch = None
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
     if p not in sys.path:
