@@ -189,7 +189,9 @@ int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first
 int nw_sha512(nw_ctx* ctx, const uint8_t* data, size_t len, uint8_t out[64]);
 int nw_sha512_many(nw_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                    size_t n, uint8_t (*out)[64]);
-/* Device-resident bulk digest: d_base/d_off/d_len/d_out are device pointers. */
+/* Device-resident bulk digest: d_base/d_off/d_len/d_out are device pointers.  One lane per message:
+ * each message is one sequential compression chain (worker batches: ~9 us per 128-B block on one
+ * lane). */
 int nw_sha512_many_dev(nw_ctx* ctx, const uint8_t* d_base, const uint64_t* d_off,
                        const uint64_t* d_len, size_t n, uint8_t* d_out64, void* stream);
 

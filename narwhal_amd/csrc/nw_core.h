@@ -417,9 +417,10 @@ NW_HD void comb_chunk_build(const uint32_t* bases, uint32_t pos, uint32_t c, uin
             }
             const fe x = fe_mul(load_fe(sl), zi);
             const fe y = fe_mul(load_fe(sl + 10), zi);
-            store_fe(sl, fe_carry(fe_add(y, x)));
-            store_fe(sl + 10, fe_sub(y, x));
-            store_fe(sl + 20, fe_mul(fe_mul(x, y), fe_from_const(FE_D2)));
+            const ge_precomp q = ge_precomp_from_affine(x, y);
+            store_fe(sl, q.ypx);
+            store_fe(sl + 10, q.ymx);
+            store_fe(sl + 20, q.xy2d);
             sl[30] = 0;
             sl[31] = 0;
         }

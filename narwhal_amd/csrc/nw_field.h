@@ -98,6 +98,15 @@ NW_HD fe fe_sub_loose(const fe& f, const fe& g) {
     return h;
 }
 
+// h = f - g without the carry pass for tight f and g (g limbs <= 2p limbs): f + 2p - g, limbs
+// < 3 * 2^26 (k = 3): still a valid second fe_mul operand (19 * 3 * 2^26 < 2^32).
+NW_HD fe fe_sub2p_loose(const fe& f, const fe& g) {
+    fe h;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] + FE_2P[i] - g.v[i];
+    return h;
+}
+
 // h = -f for tight f, k = 2 output (no carry): 2p - f.
 NW_HD fe fe_neg(const fe& f) {
     fe h;
@@ -127,6 +136,23 @@ NW_HD fe fe_reduce_wide(uint64_t h[10]) {
     return r;
 }
 
+// 2x as an addition: on gfx950 v_add_u32 issues at the full rate, the v_lshlrev_b32 the compiler
+// picks for 2 * x at half rate (profiles/r01/isa/isa_rates_vop2.jsonl).  Off by default: it removes
+// 35 of 1,264 VALU instructions per comb step but measured no faster at C2 (k_verify 1.188 vs
+// 1.181 ms, profiles/r02/ab_r02d.txt) — the loop is bound by v_mad_u64_u32 issue, not by these.
+#ifndef NW_ADD_DBL
+#define NW_ADD_DBL 0
+#endif
+NW_HD uint32_t dbl32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__) && NW_ADD_DBL
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
+    return r;
+#else
+    return 2u * x;
+#endif
+}
+
 // h = f * g mod p.  Coefficient of f_i g_j: 2 if i, j both odd; x19 if i + j >= 10.
 NW_HD fe fe_mul(const fe& f, const fe& g) {
     uint32_t g19[10];
@@ -134,7 +160,7 @@ NW_HD fe fe_mul(const fe& f, const fe& g) {
     for (int j = 0; j < 10; ++j) g19[j] = 19u * g.v[j];
     uint32_t f2[10];
 #pragma unroll
-    for (int i = 0; i < 10; ++i) f2[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
+    for (int i = 0; i < 10; ++i) f2[i] = (i & 1) ? dbl32(f.v[i]) : f.v[i];
     uint64_t acc[10];
 #pragma unroll
     for (int k = 0; k < 10; ++k) acc[k] = 0;

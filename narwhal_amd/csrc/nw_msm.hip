@@ -66,18 +66,16 @@ NW_HD ge_p3 ge_dbl_xyz(const ge_p3& p) {
     return r;
 }
 
-// Affine Niels entry of a decompressed (Z = 1) point, in the 128-B table-entry layout.
+// Table-entry (halved affine Niels) form of a decompressed (Z = 1) point, 128-B layout.
 NW_HD void store_niels_affine(uint32_t* dst, const ge_p3& p) {
-    const fe ypx = fe_carry(fe_add(p.Y, p.X));
-    const fe ymx = fe_sub(p.Y, p.X);
-    const fe xy2d = fe_mul(p.T, fe_from_const(FE_D2));
+    const ge_precomp e = ge_precomp_from_affine(p.X, p.Y);
     uint4* q = reinterpret_cast<uint4*>(dst);
     uint32_t w[32];
 #pragma unroll
     for (int k = 0; k < 10; ++k) {
-        w[k] = ypx.v[k];
-        w[10 + k] = ymx.v[k];
-        w[20 + k] = xy2d.v[k];
+        w[k] = e.ypx.v[k];
+        w[10 + k] = e.ymx.v[k];
+        w[20 + k] = e.xy2d.v[k];
     }
     w[30] = 0;
     w[31] = 0;

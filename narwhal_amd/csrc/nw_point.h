@@ -1,7 +1,8 @@
 // edwards25519 group arithmetic for gfx950 (twisted Edwards, a = -1).
 //
 //   ge_p3      extended (X:Y:Z:T), x = X/Z, y = Y/Z, xy = T/Z
-//   ge_precomp affine Niels (y+x, y-x, 2dxy): fixed-base table entries, 7M mixed addition
+//   ge_precomp affine Niels, HALVED ((y+x)/2, (y-x)/2, d xy): fixed-base table entries and MSM
+//              bucket entries, 7M mixed addition (see ge_madd for why halved)
 //   ge_cached  projective Niels (Y+X, Y-X, Z, 2dT): variable-base operands, 8M addition
 //
 // All formulas are the complete unified ones (Hisil-Wong-Carter-Dawson 2008), so results are the
@@ -24,7 +25,10 @@ struct ge_cached {
 };
 
 // Table entry layout in HBM: 32 u32 words = 128 B (one cache line):
-//   [0..9] y+x, [10..19] y-x, [20..29] 2dxy, [30..31] zero pad.
+//   [0..9] (y+x)/2, [10..19] (y-x)/2, [20..29] d x y, [30..31] zero pad.
+#ifndef NW_HALF_NIELS
+#define NW_HALF_NIELS 1
+#endif
 static constexpr int PRECOMP_WORDS = 32;
 // Fixed-base combs: signed radix-2^W digits, one table per digit position holding the multiples
 // |d| * 2^(W*pos) * P for |d| = 0..2^(W-1) (0 = identity).  W = 24 for the basepoint (11 positions,
@@ -50,12 +54,54 @@ NW_HD ge_p3 ge_identity() {
 
 NW_HD ge_precomp ge_precomp_identity() {
     ge_precomp r;
+#if NW_HALF_NIELS
+    r.ypx = fe_from_const(FE_HALF);
+    r.ymx = fe_from_const(FE_HALF);
+#else
     r.ypx = fe_one();
     r.ymx = fe_one();
+#endif
     r.xy2d = fe_zero();
     return r;
 }
 
+#if NW_HALF_NIELS
+// p + q (mixed, halved entry).  The HWCD formulas with every quantity halved: A/2 = (Y1-X1)(y-x)/2,
+// B/2, C/2 = T1 d x y, D/2 = Z1 (no doubling), E/2, F/2 = Z1 - C/2, G/2, H/2; the products
+// E F, G H, G F, E H are the sum times 1/4 in every coordinate, i.e. the same projective point.
+// Halving the table entries once at build time removes the 2 Z1 addition and the carry pass of F
+// from every addition: F/2 = Z1 + 2p - C/2 has limbs < 3 * 2^26 (k = 3), so it is a valid second
+// fe_mul operand (19 F/2 < 2^32) without carrying.  Limb budget: (Y1+X1) k=2, (Y1-X1) and
+// e = b - a loose (k = 5, first operands only), f k=3, g = Z1 + C/2 k=2, h = b + a k=2; products
+// e f 15, g h 4, g f 6, e h 10 <= 32.  xy2d (d x y) may be k=2 (negated entry).
+NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) {
+    const fe a = fe_mul(fe_sub_loose(p.Y, p.X), q.ymx);
+    const fe b = fe_mul(fe_add(p.Y, p.X), q.ypx);
+    const fe c = fe_mul(p.T, q.xy2d);
+    const fe e = fe_sub_loose(b, a);
+    const fe h = fe_add(b, a);
+    const fe f = fe_sub2p_loose(p.Z, c);
+    const fe g = fe_add(p.Z, c);
+    ge_p3 r;
+    r.X = fe_mul(e, f);
+    r.Y = fe_mul(g, h);
+    r.Z = fe_mul(g, f);
+    r.T = fe_mul(e, h);
+    return r;
+}
+
+// Extended point of a halved affine Niels entry, with no field multiplication beyond T:
+// X = (y+x)/2 - (y-x)/2 = x, Y = y, Z = 1, T = xy = (d x y) / d.
+// Starts a comb chain without the 7-multiplication addition to the identity.
+NW_HD ge_p3 ge_from_precomp(const ge_precomp& q) {
+    ge_p3 r;
+    r.X = fe_sub(q.ypx, q.ymx);
+    r.Y = fe_carry(fe_add(q.ypx, q.ymx));
+    r.Z = fe_one();
+    r.T = fe_mul(q.xy2d, fe_from_const(FE_INVD));
+    return r;
+}
+#else
 // p + q (mixed).  Limb budget: (Y1+X1) k=2, D = 2Z1 k=2, G = D + C k=3, xy2d may be k=2 (negated).
 // (Y1-X1) and e = b - a skip the carry pass (fe_sub_loose, k = 5): each only ever feeds fe_mul as
 // the first operand against a second operand of k <= 2 (ymx tight; f tight; h k=2): 5 x 2 <= 32.
@@ -76,9 +122,7 @@ NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) {
     return r;
 }
 
-// Extended point of an affine Niels entry, with no field multiplication beyond T:
-// X = (y+x) - (y-x) = 2x, Y = (y+x) + (y-x) = 2y, Z = 2, T = 2xy = (2dxy) / d.
-// Starts a comb chain without the 7-multiplication addition to the identity.
+// X = (y+x) - (y-x) = 2x, Y = 2y, Z = 2, T = 2xy = (2dxy) / d.
 NW_HD ge_p3 ge_from_precomp(const ge_precomp& q) {
     ge_p3 r;
     r.X = fe_sub(q.ypx, q.ymx);
@@ -87,6 +131,24 @@ NW_HD ge_p3 ge_from_precomp(const ge_precomp& q) {
     r.Z.v[0] = 2;
     r.T = fe_mul(q.xy2d, fe_from_const(FE_INVD));
     return r;
+}
+#endif
+
+// Table-entry form of affine (x, y) (tight limbs): halved affine Niels, or plain when
+// NW_HALF_NIELS is 0.
+NW_HD ge_precomp ge_precomp_from_affine(const fe& x, const fe& y) {
+    ge_precomp q;
+#if NW_HALF_NIELS
+    const fe half = fe_from_const(FE_HALF);
+    q.ypx = fe_mul(fe_add(y, x), half);
+    q.ymx = fe_mul(fe_sub(y, x), half);
+    q.xy2d = fe_mul(fe_mul(x, y), fe_from_const(FE_D));
+#else
+    q.ypx = fe_carry(fe_add(y, x));
+    q.ymx = fe_sub(y, x);
+    q.xy2d = fe_mul(fe_mul(x, y), fe_from_const(FE_D2));
+#endif
+    return q;
 }
 
 NW_HD ge_cached ge_to_cached(const ge_p3& p) {
@@ -233,16 +295,10 @@ NW_HD ge_precomp ge_precomp_from_words(const uint32_t* w) {
     return q;
 }
 
-// Affine Niels form of p (one inversion); tight limbs.
+// Table-entry (halved affine Niels) form of p (one inversion); tight limbs.
 NW_HD ge_precomp ge_to_precomp(const ge_p3& p) {
     const fe zi = fe_invert_sg(p.Z);
-    const fe x = fe_mul(p.X, zi);
-    const fe y = fe_mul(p.Y, zi);
-    ge_precomp q;
-    q.ypx = fe_carry(fe_add(y, x));
-    q.ymx = fe_sub(y, x);
-    q.xy2d = fe_mul(fe_mul(x, y), fe_from_const(FE_D2));
-    return q;
+    return ge_precomp_from_affine(fe_mul(p.X, zi), fe_mul(p.Y, zi));
 }
 
 // Signed radix-2^W recoding, consumed one digit per call: s holds the remaining scalar bits

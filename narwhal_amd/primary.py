@@ -384,8 +384,9 @@ def verify_certificates(certs: Sequence[Certificate], committee: Committee, engi
             out[i] = MalformedHeader(h.id.hex())
         else:
             live.append(i)
-    # header signatures: one strict-verify submission
+    # header signatures: one strict-verify submission (committee keys cached first: comb path)
     if live:
+        committee_slots(eng, committee)
         ok = eng.verify_strict_many([certs[i].header.id for i in live], [certs[i].header.author for i in live],
                                     [certs[i].header.signature for i in live])
         nxt = []

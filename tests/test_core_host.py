@@ -23,6 +23,18 @@ class OracleEngine:
         self.calls.append("verify_strict_many")
         return [o.verify_strict(k, m, s) for m, k, s in zip(msgs, pks, sigs)]
 
+    def committee_load(self, keys, stakes=None):
+        self.keys = list(keys)
+        return list(range(len(self.keys)))
+
+    def verify_certs(self, ranges, sigs_blob, signer, msgs_blob, zseed, cert_base=0):
+        self.calls.append("verify_certs")
+        ok = []
+        for c, (f, n) in enumerate(ranges):
+            votes = [(self.keys[signer[f + v]], sigs_blob[64 * (f + v):64 * (f + v + 1)]) for v in range(n)]
+            ok.append(o.crypto_verify_batch(msgs_blob[32 * c:32 * (c + 1)], votes, zseed, cert_base + c))
+        return ok, None, None
+
 
 @pytest.fixture(scope="module")
 def world():
@@ -110,3 +122,50 @@ def test_core_batcher_votes_to_certificate(world):
     assert b.gc_round == 10
     errs, _, _ = b.submit([_header(seeds, keys, 1, 9)])
     assert isinstance(errs[0], core.TooOld)
+
+
+def test_pipeline_equals_sequential_submit_and_overlaps(world):
+    """CoreBatcher.pipeline: batch k+1's checks start before batch k is applied, the state changes
+    made between batches (set_current_header, advance_gc) are honoured, and every result equals
+    submit() called batch after batch."""
+    seeds, keys, com = world
+    h3 = _header(seeds, keys, 0, 3)
+    h4 = _header(seeds, keys, 0, 4)
+    c3 = [pm.Certificate(_header(seeds, keys, a, 3),
+                         [(keys[i], o.sign(seeds[i], o.digest32(pm.Vote(_header(seeds, keys, a, 3).id, 3, keys[a],
+                                                                          keys[0]).digest_preimage())))
+                          for i in range(3)]) for a in (1, 2, 3)]
+    batches = [
+        [_vote(seeds, keys, h3, 1), _vote(seeds, keys, h3, 2), c3[0]],
+        [_vote(seeds, keys, h3, 3), _vote(seeds, keys, h4, 1), c3[1], _header(seeds, keys, 2, 4)],
+        [_vote(seeds, keys, h4, 1), _vote(seeds, keys, h4, 2), _vote(seeds, keys, h4, 3), c3[2]],
+        [_header(seeds, keys, 3, 1)],
+    ]
+
+    def state(k, b):
+        if k == 0:
+            b.set_current_header(h3)
+        if k == 2:
+            b.set_current_header(h4)
+        if k == 3:
+            b.advance_gc(55)
+
+    seq = core.CoreBatcher(com, engine=OracleEngine())
+    want = []
+    for k, msgs in enumerate(batches):
+        state(k, seq)
+        want.append(seq.submit(msgs, zseed=bytes(32)))
+    pip = core.CoreBatcher(com, engine=OracleEngine())
+    pip.trace = []
+    got = list(pip.pipeline(batches, zseed=bytes(32), before_apply=state))
+    norm = lambda r: ([type(e) if e else None for e in r[0]], [c.header.id for c in r[1]],
+                      [([c.origin() for c in ps], rd) for ps, rd in r[2]])
+    assert [norm(r) for r in got] == [norm(r) for r in want]
+    kinds = [norm(r)[0] for r in got]
+    assert kinds[1][1] is core.UnexpectedVote and kinds[3] == [core.TooOld]
+    assert len(got[0][1]) == 0 and len(got[1][1]) == 1 and len(got[2][1]) == 1
+    ev = pip.trace
+    for k in range(len(batches) - 1):
+        # batch k+1 is handed to the GPU worker before batch k is applied (deterministic order)
+        assert ev.index(("submitted", k + 1)) < ev.index(("apply_done", k))
+        assert ev.index(("check_done", k)) < ev.index(("apply_done", k))

@@ -217,3 +217,32 @@ def test_worker_batch_digests_vs_hashlib(engine, n_tx, tx_size):
     got = engine.sha512_many([bytes(b) for b in host])
     assert got == [hashlib.sha512(bytes(b)).digest() for b in host]
     assert engine.sha512(bytes(host[0])) == hashlib.sha512(bytes(host[0])).digest()
+
+
+
+def test_sha512_many_mixed_lengths_unaligned(engine):
+    """k_sha512_many on mixed lengths (empty, sub-block, 111/112/128-B boundaries, a worker batch)
+    at unaligned offsets, through the device entry point, vs hashlib."""
+    import torch
+    rng = np.random.default_rng(17)
+    lens = [0, 1, 111, 112, 127, 128, 129, 239, 240, 255, 256, 5000, 70001, 508052] + \
+        [int(x) for x in rng.integers(0, 20000, size=120)]
+    msgs = [rng.integers(0, 256, size=n, dtype=np.uint8).tobytes() for n in lens]
+    offs, pos = [], 3                  # start unaligned
+    for m in msgs:
+        offs.append(pos)
+        pos += len(m) + int(rng.integers(0, 5))
+    blob = np.zeros(pos + 16, np.uint8)
+    for o, m in zip(offs, msgs):
+        blob[o:o + len(m)] = np.frombuffer(m, np.uint8)
+    dev = torch.device("cuda", 0)
+    d_blob = torch.from_numpy(blob).to(dev)
+    d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    d_len = torch.tensor(lens, dtype=torch.int64, device=dev)
+    d_out = torch.zeros((len(msgs), 64), dtype=torch.uint8, device=dev)
+    engine.sha512_many_dev(d_blob.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), len(msgs), d_out.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy()
+    bad = [i for i, m in enumerate(msgs) if bytes(got[i]) != hashlib.sha512(m).digest()]
+    assert not bad, [(i, lens[i]) for i in bad[:10]]

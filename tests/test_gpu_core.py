@@ -31,39 +31,58 @@ def _cert(seeds, keys, h, voters):
     return pm.Certificate(h, [(keys[i], o.sign(seeds[i], d)) for i in voters])
 
 
-def _serial(msg, com, gc_round, current, engine, zseed, cert_index):
-    """One message through the one-message verify forms, in the reference's order."""
-    try:
-        if isinstance(msg, pm.Header):
-            if gc_round > msg.round:
-                return core.TooOld
-            msg.verify(com, engine)
-        elif isinstance(msg, pm.Vote):
-            if current.round > msg.round:
-                return core.TooOld
-            if not (msg.id == current.id and msg.origin == current.author and msg.round == current.round):
-                return core.UnexpectedVote
-            msg.verify(com, engine)
-        else:
-            if gc_round > msg.round():
-                return core.TooOld
-            # honest / corrupted votes: the verdict does not depend on the batch coefficients
-            errs = pm.verify_certificates([msg], com, engine, zseed, cert_index)
-            if errs[0] is not None:
-                raise errs[0]
-    except pm.DagError as e:
-        return type(e)
-    return None
+def _oracle(msg, com, gc_round, current, zseed, cert_index):
+    """Expected verdict of one message from the ORACLE (no GPU in the loop): the Core::sanitize_*
+    check order (primary/src/core.rs:306-346, messages.rs:48-67,131-142,189-215) with the crypto of
+    oracle/ed25519_oracle.py.  Batch coefficients: the certificate's index in the submission (the
+    corrupted votes used here are rejected under any coefficients)."""
+    def header_err(h):
+        if o.digest32(h.digest_preimage()) != h.id:
+            return pm.InvalidHeaderId
+        if com.stake(h.author) <= 0:
+            return pm.UnknownAuthority
+        if any(not com.has_worker(h.author, w) for w in h.payload.values()):
+            return pm.MalformedHeader
+        if not o.verify_strict(h.author, h.id, h.signature):
+            return pm.InvalidSignature
+        return None
+
+    if isinstance(msg, pm.Header):
+        return core.TooOld if gc_round > msg.round else header_err(msg)
+    if isinstance(msg, pm.Vote):
+        if current.round > msg.round:
+            return core.TooOld
+        if not (msg.id == current.id and msg.origin == current.author and msg.round == current.round):
+            return core.UnexpectedVote
+        if com.stake(msg.author) <= 0:
+            return pm.UnknownAuthority
+        return None if o.verify_strict(msg.author, o.digest32(msg.digest_preimage()), msg.signature) \
+            else pm.InvalidSignature
+    if gc_round > msg.round():
+        return core.TooOld
+    if msg.is_genesis(com):
+        return None
+    e = header_err(msg.header)
+    if e is not None:
+        return e
+    used, weight = set(), 0
+    for k, _ in msg.votes:
+        if k in used:
+            return pm.AuthorityReuse
+        if com.stake(k) <= 0:
+            return pm.UnknownAuthority
+        used.add(k)
+        weight += com.stake(k)
+    if weight < com.quorum_threshold():
+        return pm.CertificateRequiresQuorum
+    ok = o.crypto_verify_batch(o.digest32(msg.digest_preimage()), msg.votes, zseed, cert_index)
+    return None if ok else pm.InvalidSignature
 
 
-def test_mixed_batch_matches_serial(engine):
-    seeds = o.reference_fixture_seeds(7)
-    keys = [o.public_from_seed(s) for s in seeds]
-    com = pm.Committee({k: (1, [0]) for k in keys})        # quorum 5 of 7
-    rng = random.Random(11)
-    own = _header(seeds, keys, 0, 8)
+def _mixed(seed, n, own, seeds, keys):
+    rng = random.Random(seed)
     msgs = []
-    for j in range(60):
+    for j in range(n):
         kind = j % 3
         r = rng.choice([3, 8, 9])
         if kind == 0:
@@ -83,15 +102,54 @@ def test_mixed_batch_matches_serial(engine):
                 k, s = c.votes[2]
                 c.votes[2] = (k, s[:40] + bytes([s[40] ^ 2]) + s[41:])
             msgs.append(c)
+    return msgs
+
+
+def test_mixed_batch_matches_oracle(engine):
+    seeds = o.reference_fixture_seeds(7)
+    keys = [o.public_from_seed(s) for s in seeds]
+    com = pm.Committee({k: (1, [0]) for k in keys})        # quorum 5 of 7
+    own = _header(seeds, keys, 0, 8)
+    msgs = _mixed(11, 60, own, seeds, keys)
     zseed = bytes(range(32))
     got = core.sanitize_messages(msgs, com, gc_round=5, current_header=own, engine=engine, zseed=zseed)
     idx, want = 0, []
     for m in msgs:
-        want.append(_serial(m, com, 5, own, engine, zseed, idx))
+        want.append(_oracle(m, com, 5, own, zseed, idx))
         idx += isinstance(m, pm.Certificate)
     assert [type(e) if e else None for e in got] == want
     kinds = set(want)
     assert {None, pm.InvalidSignature, core.TooOld, core.UnexpectedVote, pm.CertificateRequiresQuorum} <= kinds
+
+
+def test_pipelined_batcher_matches_oracle(engine):
+    """CoreBatcher.pipeline on the GPU: 4 batches, the next one checked while the previous one's
+    verdicts are applied; every verdict equals the oracle's for the state at apply time."""
+    seeds = o.reference_fixture_seeds(7)
+    keys = [o.public_from_seed(s) for s in seeds]
+    com = pm.Committee({k: (1, [0]) for k in keys})
+    own = _header(seeds, keys, 0, 8)
+    batches = [_mixed(100 + k, 30, own, seeds, keys) for k in range(4)]
+    zseed = bytes(range(32))
+    b = core.CoreBatcher(com, engine=engine)
+    b.trace = []
+
+    def state(k, bb):
+        if k == 0:
+            bb.set_current_header(own)
+        if k == 2:
+            bb.advance_gc(54)            # gc_round 4 from batch 2 on
+
+    got = list(b.pipeline(batches, zseed=zseed, before_apply=state))
+    for k, (errs, _, _) in enumerate(got):
+        gc = 4 if k >= 2 else 0
+        want = [_oracle(m, com, gc, own, zseed, 0) for m in batches[k]]
+        got_k = [type(e) if e else None for e in errs]
+        # AuthorityReuse comes from the votes aggregator (apply step), not from sanitize
+        assert [g for g, w in zip(got_k, want) if g is not pm.AuthorityReuse or w is not None] == \
+            [w for g, w in zip(got_k, want) if g is not pm.AuthorityReuse or w is not None], k
+    for k in range(3):
+        assert b.trace.index(("submitted", k + 1)) < b.trace.index(("apply_done", k))
 
 
 def test_batcher_assembles_and_hands_parents(engine):
