@@ -36,9 +36,12 @@ struct KeyHash {
     }
 };
 
-// base64 0.13 STANDARD decoding (crypto/src/lib.rs:73): alphabet A-Z a-z 0-9 + /, optional '='
-// padding only at the end and only as much as completes the last quantum, a 1-symbol final
-// quantum rejected (InvalidLength), non-zero trailing bits rejected (InvalidLastSymbol).
+// base64 0.13 STANDARD decoding (crypto/src/lib.rs:73), restated from the published crate's
+// decode_suffix (not vendored here: parity unpinned, tests/golden/README.md): alphabet A-Z a-z 0-9
+// + /; '=' is padding only in the final quantum, only at positions 2 and 3 of a quad (counted
+// from the start of the string) and with nothing but '=' after it; padding is NOT required to
+// complete the quad (46 symbols + one '=' decodes) and may be absent; a final quantum of one
+// symbol is InvalidLength; non-zero trailing bits of the last symbol are InvalidLastSymbol.
 int b64val(uint8_t c) {
     if (c >= 'A' && c <= 'Z') return c - 'A';
     if (c >= 'a' && c <= 'z') return c - 'a' + 26;
@@ -49,12 +52,12 @@ int b64val(uint8_t c) {
 }
 
 bool b64_decode(const uint8_t* s, size_t n, std::vector<uint8_t>& out) {
-    size_t pad = 0;
-    while (pad < n && pad < 2 && s[n - 1 - pad] == '=') ++pad;
-    const size_t m = n - pad;   // symbols
-    if (pad && (n % 4) != 0) return false;
+    size_t m = 0;                 // symbols before the first '='
+    while (m < n && s[m] != '=') ++m;
+    for (size_t i = m; i < n; ++i)   // padding: only '=', each at quad position 2 or 3
+        if (s[i] != '=' || i % 4 < 2) return false;
+    if (n - m > 2) return false;
     if (m % 4 == 1) return false;
-    if (pad && (m % 4) + pad != 4) return false;
     out.clear();
     out.reserve(m * 3 / 4);
     uint32_t acc = 0;

@@ -122,21 +122,21 @@ _B64 = b"ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/"
 
 def _b64_decode(s: bytes) -> Optional[bytes]:
     """base64 0.13 STANDARD decode (crypto/src/lib.rs:73) as restated in nw_primary.cpp b64_decode:
-    '=' padding optional but, when present, only at the end completing the last quantum; a
-    1-symbol final quantum and non-zero trailing bits are rejected.  None = decode error."""
+    '=' only in the final quantum at quad positions 2 and 3 with nothing but '=' after it, padding
+    optional and not required to complete the quad; a 1-symbol final quantum and non-zero trailing
+    bits are rejected.  None = decode error."""
+    s = bytes(s)
     n = len(s)
-    pad = 0
-    while pad < min(n, 2) and s[n - 1 - pad:n - pad] == b"=":
-        pad += 1
-    m = n - pad
-    if (pad and n % 4) or m % 4 == 1 or (pad and m % 4 + pad != 4):
+    m = s.find(b"=")
+    m = n if m < 0 else m
+    if any(s[i:i + 1] != b"=" or i % 4 < 2 for i in range(m, n)) or n - m > 2 or m % 4 == 1:
         return None
     if any(c not in _B64 for c in s[:m]):
         return None
-    full = bytes(s[:m]) + b"=" * (-m % 4)
+    full = s[:m] + b"=" * (-m % 4)
     out = base64.b64decode(full)
     # trailing bits of the last symbol must be zero (re-encoding reproduces the symbols)
-    if base64.b64encode(out)[:m] != bytes(s[:m]):
+    if base64.b64encode(out)[:m] != s[:m]:
         return None
     return out
 

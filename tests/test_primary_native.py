@@ -152,7 +152,7 @@ def test_truncations_and_variants(golden):
 
 
 @pytest.mark.parametrize("variant", ["canonical", "unpadded", "bad_pad", "trailing_bits", "bad_char", "short",
-                                     "long", "one_symbol_tail", "pad_in_middle"])
+                                     "long", "one_symbol_tail", "pad_in_middle", "partial_pad", "over_pad"])
 def test_base64_public_keys(golden, variant):
     """base64 0.13 decode rules (crypto/src/lib.rs:73-79); native decoder == Python mirror.  No
     reference vectors exist for malformed keys: these verdicts are parity unpinned."""
@@ -162,7 +162,11 @@ def test_base64_public_keys(golden, variant):
     s = {"canonical": enc, "unpadded": enc[:-1], "bad_pad": enc + b"=",
          "trailing_bits": enc[:42] + bytes([enc[42] + 1]) + b"=", "bad_char": b"*" + enc[1:],
          "short": base64.b64encode(k[:31]), "long": base64.b64encode(k + b"\x01\x02\x03"),
-         "one_symbol_tail": enc[:-1] + b"AA", "pad_in_middle": enc[:20] + b"=" + enc[21:]}[variant]
+         "one_symbol_tail": enc[:-1] + b"AA", "pad_in_middle": enc[:20] + b"=" + enc[21:],
+         # 34 bytes = 46 symbols + "==": base64 0.13 accepts a quad completed by only one '='
+         "partial_pad": base64.b64encode(k + b"\x07\x00")[:-1],
+         # 35 bytes = 47 symbols + "=": a second '=' lands on quad position 0
+         "over_pad": base64.b64encode(k + b"\x07\x00\x01") + b"="}[variant]
     cert = _fixture_cert(golden)
     votes = [(base64.b64encode(kk), sg) for kk, sg in cert.votes]
     votes[1] = (s, votes[1][1])
@@ -170,10 +174,22 @@ def test_base64_public_keys(golden, variant):
     frame = _raw_cert_frame(base64.b64encode(h.author), h.round, [], sorted(h.parents), h.id, h.signature, votes)
     _check_against_python([frame], com)
     v = pm.decode_certificate_frames([frame], com).view(0)
-    ok = variant in ("canonical", "unpadded", "long")
+    ok = variant in ("canonical", "unpadded", "long", "partial_pad")
     assert (v["status"] == _lib.DAG_PENDING) == ok
     if ok:
         assert v["votes"][1][0] == k
+
+
+def test_b64_decode_rules():
+    """The restated base64 0.13 decode_suffix rules on short strings (Python mirror; the native
+    decoder agrees through test_base64_public_keys).  Parity unpinned: the crate is not vendored."""
+    from narwhal_amd.primary import _b64_decode
+    cases = {b"": b"", b"AA": b"\x00", b"AA=": b"\x00", b"AA==": b"\x00", b"AAA": b"\x00\x00",
+             b"AAA=": b"\x00\x00", b"AAAA": b"\x00" * 3, b"A": None, b"A=": None, b"A==": None,
+             b"AAA==": None, b"AA===": None, b"=": None, b"AB": None, b"AAB": None, b"AA=A": None,
+             b"AAAAA": None, b"QQ": b"A", b"QUI": b"AB", b"AA*A": None}
+    for s, want in cases.items():
+        assert _b64_decode(s) == want, s
 
 
 def test_host_check_order(golden):
