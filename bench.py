@@ -85,6 +85,16 @@ def host_cores():
     return len(os.sched_getaffinity(0))
 
 
+def cgroup_cpu_quota():
+    """CPUs the container's cgroup may use (cpu.max quota / period), or None when unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -120,6 +130,9 @@ def cpu_baseline(cs, com, seconds):
             "per_gpu_share": {"value": rate / GPUS_PER_NODE, "cores": threads / GPUS_PER_NODE,
                               "note": "host rate / %d GPUs per node" % GPUS_PER_NODE},
             "cpu_model": cpu_model(),
+            # the affinity mask can be far wider than the cgroup's CPU quota (GPU box: 256 vs 16);
+            # threads beyond the quota time-slice, tools/cpu_probe.py -> profiles/r02/cpu_probe_r02.json
+            "cgroup_cpu_quota": cgroup_cpu_quota(),
             "sample": "%d certificates x %d votes of the C2 workload (%d sigs) in %.1f s on %d threads; "
                       "oracle/nw_ref.c (C restatement of ed25519-dalek 1.0.1 u64 backend: per-vote A "
                       "decompression + Straus MSM, as crypto/src/lib.rs:206-219)"

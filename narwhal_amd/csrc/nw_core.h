@@ -49,6 +49,34 @@ NW_HD ge_p3 load_p3(const uint32_t* src) {
     return p;
 }
 
+__device__ __forceinline__ ge_p3 ge_shfl_down(const ge_p3& p, unsigned off) {
+    ge_p3 r;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        r.X.v[k] = __shfl_down(p.X.v[k], off, 64);
+        r.Y.v[k] = __shfl_down(p.Y.v[k], off, 64);
+        r.Z.v[k] = __shfl_down(p.Z.v[k], off, 64);
+        r.T.v[k] = __shfl_down(p.T.v[k], off, 64);
+    }
+    return r;
+}
+
+// Moves a wave-uniform point into VGPRs behind an optimizer barrier.  Without it the serial chains
+// of k_msm_final / k_points_identity / k_cert_finalize (uniform: one batch per wave) are scalarized onto the SALU,
+// which has no 32x32->64 multiply-add: PMC showed 800 k SALU vs 61 k VALU instructions per wave
+// and 1.6 ms per k_msm_final launch.
+__device__ __forceinline__ ge_p3 ge_to_vgpr(ge_p3 p) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        asm volatile("" : "+v"(p.X.v[k]));
+        asm volatile("" : "+v"(p.Y.v[k]));
+        asm volatile("" : "+v"(p.Z.v[k]));
+        asm volatile("" : "+v"(p.T.v[k]));
+    }
+    return p;
+}
+
+
 // Byte of the virtual hram stream (R || A || M) at position pos >= 64, with SHA padding.
 NW_HD uint32_t stream_byte(const uint8_t* msg, uint64_t len, uint64_t pos) {
     const uint64_t m = pos - 64;

@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
 // Per-certificate verdict: definitive Err on any bad S / undecodable A / undecodable R, else the
 // exact remaining batch sum (usually empty) must be the identity.  One 64-lane wave per
 // certificate: lanes stride over the votes (coalesced flag reads), wave reductions combine them;
-// the exact sum over slow-path terms (failing certificates only) runs on lane 0.
+// the exact sum over slow-path terms (failing certificates only) is a lane-strided sum + shuffle tree.
 __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
@@ -196,25 +196,27 @@ __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
         tsum += __shfl_xor(tsum, off, 64);
         stake += __shfl_xor(stake, off, 64);
     }
-    if (lane != 0) return;
     bool ok;
     if (bad) {
         ok = false;
     } else if (!slow) {
         ok = (tsum & 7u) == 0;
     } else {
-        ge_p3 acc = ge_identity();
-        for (uint32_t v = 0; v < nv; ++v) {
-            const uint32_t f = a.flags[first + v];
-            if (f & NW_F_SLOW) {
+        // exact sum of the slow-path terms: lanes stride over the votes, then a shuffle tree
+        ge_p3 acc = ge_to_vgpr(ge_identity());
+        for (uint32_t v = lane; v < nv; v += 64) {
+            if (a.flags[first + v] & NW_F_SLOW) {
                 const ge_p3 Q = load_p3(a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS);
                 acc = ge_add(acc, ge_to_cached(Q));
             }
         }
+#pragma unroll
+        for (unsigned off = 32; off > 0; off >>= 1) acc = ge_add(acc, ge_to_cached(ge_shfl_down(acc, off)));
         const ge_cached t8c = ge_to_cached(ge_t8());
         for (uint32_t k = 0; k < (tsum & 7u); ++k) acc = ge_add(acc, t8c);
         ok = ge_is_identity(acc);
     }
+    if (lane != 0) return;
     if (a.cert_ok) a.cert_ok[c] = ok ? 1 : 0;
     if (a.accepted_stake) a.accepted_stake[c] = stake;
 }

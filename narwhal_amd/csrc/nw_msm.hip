@@ -83,18 +83,6 @@ NW_HD void store_niels_affine(uint32_t* dst, const ge_p3& p) {
     for (int k = 0; k < 8; ++k) q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
 
-__device__ __forceinline__ ge_p3 ge_shfl_down(const ge_p3& p, unsigned off) {
-    ge_p3 r;
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        r.X.v[k] = __shfl_down(p.X.v[k], off, 64);
-        r.Y.v[k] = __shfl_down(p.Y.v[k], off, 64);
-        r.Z.v[k] = __shfl_down(p.Z.v[k], off, 64);
-        r.T.v[k] = __shfl_down(p.T.v[k], off, 64);
-    }
-    return r;
-}
-
 NW_HD ge_p3 ge_add_p3(const ge_p3& a, const ge_p3& b) { return ge_add(a, ge_to_cached(b)); }
 
 // k * Q for k < 2^253 (8 LE words): signed radix-16 digits, most significant first.  The multiples
@@ -433,7 +421,7 @@ __global__ void __launch_bounds__(64) k_msm_final(MsmParams a, const uint32_t* w
 #pragma unroll
         for (unsigned off = 32; off > 0; off >>= 1) col[k] += __shfl_xor(col[k], off, 64);
     }
-    if (L != 0) return;
+    // every lane runs the serial tail (the values are VGPR-resident, see ge_to_vgpr); lane 0 stores
     // sum_i z_i s_i < n 2^381 < 2^413: 16 words, then mod l
     uint32_t x[16];
     uint64_t carry = 0;
@@ -445,7 +433,7 @@ __global__ void __launch_bounds__(64) k_msm_final(MsmParams a, const uint32_t* w
     }
     uint32_t bc[8];
     sc_reduce512(bc, x);
-    ge_p3 acc = load_p3(wsum + ((size_t)b * NA + NA - 1) * MSM_PT_WORDS);
+    ge_p3 acc = ge_to_vgpr(load_p3(wsum + ((size_t)b * NA + NA - 1) * MSM_PT_WORDS));
 #pragma nounroll
     for (int j = NA - 2; j >= 0; --j) {
 #pragma unroll
@@ -456,16 +444,20 @@ __global__ void __launch_bounds__(64) k_msm_final(MsmParams a, const uint32_t* w
     uint32_t zero8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     const ge_p3 PB = comb_sB_minus_hA<B_WINDOW, 0>(bc, zero8, a.btab, nullptr);
     acc = ge_add(acc, ge_cached_neg(ge_to_cached(PB)));
+    if (L != 0) return;
     if (a.point_out) store_p3(a.point_out + (size_t)b * MSM_PT_WORDS, acc);
     if (a.batch_ok) a.batch_ok[b] = (!a.bad[b] && ge_is_identity(acc)) ? 1 : 0;
 }
 
 // Sum of npts extended points (the shards of one split batch) == identity.
 __global__ void __launch_bounds__(64) k_points_identity(uint32_t npts, const uint32_t* pts, uint8_t* out) {
-    if (threadIdx.x != 0) return;
-    ge_p3 acc = ge_identity();
-    for (uint32_t k = 0; k < npts; ++k) acc = ge_add_p3(acc, load_p3(pts + (size_t)k * MSM_PT_WORDS));
-    out[0] = ge_is_identity(acc) ? 1 : 0;
+    // lanes stride over the points, then a shuffle tree (all values in VGPRs)
+    const uint32_t L = threadIdx.x;
+    ge_p3 acc = ge_to_vgpr(ge_identity());
+    for (uint32_t k = L; k < npts; k += 64) acc = ge_add_p3(acc, load_p3(pts + (size_t)k * MSM_PT_WORDS));
+#pragma unroll
+    for (unsigned off = 32; off > 0; off >>= 1) acc = ge_add_p3(acc, ge_shfl_down(acc, off));
+    if (L == 0) out[0] = ge_is_identity(acc) ? 1 : 0;
 }
 
 template <int C>
