@@ -139,7 +139,7 @@ def cpu_baseline(cs, com, seconds):
                       % (done_certs, int(cs.cert_n[0]), done_sigs, dt, threads)}
 
 
-def host_fed(eng, cs, slots, zseed, chunks=8, threads=4):
+def host_fed(eng, cs, slots, zseed, chunks=8, threads=4, reps=5):
     """C2 through nw_verify_certs from host buffers: ``chunks`` calls over ``threads`` host threads,
     so one call's host->device copy overlaps another's kernels (each call has its own stream)."""
     from concurrent.futures import ThreadPoolExecutor
@@ -157,13 +157,18 @@ def host_fed(eng, cs, slots, zseed, chunks=8, threads=4):
 
     with ThreadPoolExecutor(threads) as ex:
         assert all(ex.map(run, parts))   # warm every workspace
-        t0 = time.perf_counter()
-        ok = all(ex.map(run, parts))
-        dt = time.perf_counter() - t0
-    assert ok
-    return {"value": cs.nsigs / dt, "unit": "sigs/s", "ms": dt * 1e3,
-            "note": "nw_verify_certs on pageable host buffers (pinned staging + one H2D/D2H per call), "
-                    "%d calls on %d threads; PCIe included" % (chunks, threads)}
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            ok = all(ex.map(run, parts))
+            ts.append(time.perf_counter() - t0)
+            assert ok
+    ts.sort()
+    dt = ts[len(ts) // 2]
+    return {"value": cs.nsigs / dt, "unit": "sigs/s", "ms": dt * 1e3, "ms_reps": [t * 1e3 for t in ts],
+            "note": "nw_verify_certs on pageable host buffers (signature arrays copied H2D directly, the rest "
+                    "staged), %d calls on %d threads, median of %d passes; PCIe and host packing included"
+                    % (chunks, threads, reps)}
 
 
 def digest_leg(eng, dev, n_node, n_share, reps, cpu_seconds, verify_step):
@@ -513,17 +518,18 @@ def main(argv=None):
             "p99_cert_latency_ms": lat[int(len(lat) * 0.99)] * 1e3 if lat else None,
             "roofline": roofline,
         }
+        # GPU legs first: the CPU baselines run more threads than the container's CPU quota, and the
+        # cgroup throttling that follows would slow the host side of the next leg
+        if world == 1 and not args.no_extras:
+            out["host_fed"] = host_fed(eng, cs, slots, zseed)
+            out["msm"] = msm_leg(eng)
+        if world == 1 and args.digest_batches > 0:
+            out["digest"] = digest_leg(eng, dev, args.digest_batches, args.digest_share, 3,
+                                       0.0 if args.no_cpu_baseline else 3.0, verify_step)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cs, com, args.cpu_seconds)
         else:
             out["cpu_baseline"] = None
-        if world == 1 and not args.no_extras:
-            out["host_fed"] = host_fed(eng, cs, slots, zseed)
-        if world == 1 and args.digest_batches > 0:
-            out["digest"] = digest_leg(eng, dev, args.digest_batches, args.digest_share, 3,
-                                       0.0 if args.no_cpu_baseline else 3.0, verify_step)
-        if world == 1 and not args.no_extras:
-            out["msm"] = msm_leg(eng)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -100,7 +100,7 @@ struct Workspace {
         w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_ok, w_misc, w_out, w_pbuf, w_pre, w_counts,
         w_cursor, w_perm, w_io, w_var, w_status, w_msm_ent, w_msm_dig, w_msm_zs, w_msm_meta, w_msm_bkt, w_msm_part,
         w_msm_wpart;
-    HostBuf h_io;
+    HostBuf h_io, h_meta;
 
     // Grow a buffer; a buffer that may still be read by a pending call is only freed after it.
     hipError_t ensure(DevBuf& b, size_t bytes) {
@@ -119,6 +119,7 @@ struct Workspace {
                           &w_msm_wpart})
             b->release();
         h_io.release();
+        h_meta.release();
     }
 };
 
@@ -515,27 +516,71 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     return NW_OK;
 }
 
-// Pack per-signature messages into the workspace (MSGMODE 1).
-int upload_messages(nw_ctx* ctx, Workspace* ws, const uint8_t* const* msg, const size_t* len, size_t n,
-                    hipStream_t st) {
-    std::vector<uint64_t> off(n), ln(n);
-    size_t total = 0;
-    for (size_t i = 0; i < n; ++i) {
-        off[i] = total;
-        ln[i] = len[i];
-        total += len[i];
+// Host-buffer inputs of one call: segments are packed into the workspace's pinned buffer (256-B
+// aligned) and copied to their device buffers with asynchronous DMAs, so a call issues no
+// pageable copies and no intermediate synchronization (the call's final stream sync releases the
+// buffer).  Segments of at least kDirectCopyBytes are copied from the caller's buffer directly:
+// the runtime's pageable H2D runs at the pinned rate (56 GB/s on MI355X) while a memcpy into the
+// staging buffer adds serial host work at 34 GB/s (tools/host_fed_probe.py).
+constexpr size_t kDirectCopyBytes = 2u << 20;
+
+class Stager {
+public:
+    Stager(Workspace* ws, hipStream_t st) : ws_(ws), st_(st) {}
+    // upper bound of the staged bytes of the call (one allocation, before any segment)
+    hipError_t reserve(size_t bytes) { return ws_->h_io.ensure(bytes + 16 * 256); }
+    static size_t room(size_t bytes) { return bytes >= kDirectCopyBytes ? 0 : align256(bytes); }
+    uint8_t* alloc(size_t n) {
+        uint8_t* h = ws_->h_io.bytes() + off_;
+        off_ = align256(off_ + n);
+        return h;
     }
-    std::vector<uint8_t> packed(total + 8);
-    for (size_t i = 0; i < n; ++i)
-        if (len[i]) std::memcpy(packed.data() + off[i], msg[i], len[i]);
+    hipError_t copy(void* dst, const uint8_t* h, size_t n) {
+        return n ? hipMemcpyAsync(dst, h, n, hipMemcpyHostToDevice, st_) : hipSuccess;
+    }
+    hipError_t put(void* dst, const void* src, size_t n) {
+        if (!n) return hipSuccess;
+        if (n >= kDirectCopyBytes) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st_);
+        uint8_t* h = alloc(n);
+        std::memcpy(h, src, n);
+        return copy(dst, h, n);
+    }
+
+private:
+    Workspace* ws_;
+    hipStream_t st_;
+    size_t off_ = 0;
+};
+
+size_t message_bytes(const size_t* len, size_t n) {
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) total += len[i];
+    return total;
+}
+
+// Staged bytes of upload_messages (the packed messages, offsets and lengths).
+size_t message_stage_bytes(size_t total, size_t n) { return align256(total + 8) + 2 * align256(n * 8 + 8); }
+
+// Pack per-signature messages into the workspace (MSGMODE 1).
+int upload_messages(nw_ctx* ctx, Workspace* ws, Stager& sg, const uint8_t* const* msg, const size_t* len, size_t n,
+                    size_t total) {
     NW_TRY(ws->ensure(ws->w_msg, total + 8), "ws msg");
     NW_TRY(ws->ensure(ws->w_msg_off, n * 8 + 8), "ws msg_off");
     NW_TRY(ws->ensure(ws->w_msg_len, n * 8 + 8), "ws msg_len");
-    NW_TRY(hipMemcpyAsync(ws->w_msg.p, packed.data(), total + 8, hipMemcpyHostToDevice, st), "H2D msg");
-    NW_TRY(hipMemcpyAsync(ws->w_msg_off.p, off.data(), n * 8, hipMemcpyHostToDevice, st), "H2D off");
-    NW_TRY(hipMemcpyAsync(ws->w_msg_len.p, ln.data(), n * 8, hipMemcpyHostToDevice, st), "H2D len");
-    // pageable sources: make sure the copies have consumed them before the vectors go away
-    NW_TRY(hipStreamSynchronize(st), "sync(messages)");
+    uint8_t* packed = sg.alloc(total + 8);
+    uint64_t* off = reinterpret_cast<uint64_t*>(sg.alloc(n * 8 + 8));
+    uint64_t* ln = reinterpret_cast<uint64_t*>(sg.alloc(n * 8 + 8));
+    size_t pos = 0;
+    for (size_t i = 0; i < n; ++i) {
+        off[i] = pos;
+        ln[i] = len[i];
+        if (len[i]) std::memcpy(packed + pos, msg[i], len[i]);
+        pos += len[i];
+    }
+    std::memset(packed + pos, 0, 8);
+    NW_TRY(sg.copy(ws->w_msg.p, packed, total + 8), "H2D msg");
+    NW_TRY(sg.copy(ws->w_msg_off.p, reinterpret_cast<uint8_t*>(off), n * 8), "H2D off");
+    NW_TRY(sg.copy(ws->w_msg_len.p, reinterpret_cast<uint8_t*>(ln), n * 8), "H2D len");
     return NW_OK;
 }
 
@@ -611,15 +656,17 @@ int enqueue_msm(nw_ctx* ctx, Workspace* ws, size_t nb, const uint32_t* counts, s
     NW_TRY(ws->ensure(ws->w_msm_bkt, ntasks * B * MSM_PT_WORDS * 4 + 16), "ws msm buckets");
     NW_TRY(ws->ensure(ws->w_msm_part, ntasks * 128 * MSM_PT_WORDS * 4 + 16), "ws msm partials");
     NW_TRY(ws->ensure(ws->w_msm_wpart, (ntasks + nb * NA) * MSM_PT_WORDS * 4 + 16), "ws msm window sums");
-    std::vector<uint8_t> hmeta(meta, 0);
-    std::memcpy(hmeta.data() + o_bfirst, bfirst.data(), nb * 4);
-    std::memcpy(hmeta.data() + o_bcount, bcount.data(), nb * 4);
-    if (nsig) std::memcpy(hmeta.data() + o_sb, sig_batch.data(), nsig * 4);
-    std::memcpy(hmeta.data() + o_wf, wfirst.data(), wfirst.size() * 4);
-    if (ntasks) std::memcpy(hmeta.data() + o_tasks, tasks.data(), ntasks * sizeof(MsmTask));
+    // staged in the workspace's second pinned buffer (every caller synchronizes before returning)
+    NW_TRY(ws->h_meta.ensure(meta), "pinned msm meta");
+    uint8_t* hmeta = ws->h_meta.bytes();
+    std::memset(hmeta, 0, meta);
+    std::memcpy(hmeta + o_bfirst, bfirst.data(), nb * 4);
+    std::memcpy(hmeta + o_bcount, bcount.data(), nb * 4);
+    if (nsig) std::memcpy(hmeta + o_sb, sig_batch.data(), nsig * 4);
+    std::memcpy(hmeta + o_wf, wfirst.data(), wfirst.size() * 4);
+    if (ntasks) std::memcpy(hmeta + o_tasks, tasks.data(), ntasks * sizeof(MsmTask));
     uint8_t* dm = ws->w_msm_meta.as<uint8_t>();
-    NW_TRY(hipMemcpyAsync(dm, hmeta.data(), meta, hipMemcpyHostToDevice, st), "H2D msm meta");
-    NW_TRY(hipStreamSynchronize(st), "sync(msm meta)");   // pageable source
+    NW_TRY(hipMemcpyAsync(dm, hmeta, meta, hipMemcpyHostToDevice, st), "H2D msm meta");
     MsmParams mp{};
     mp.nb = (uint32_t)nb;
     mp.nsig = (uint32_t)nsig;
@@ -656,12 +703,15 @@ int enqueue_msm(nw_ctx* ctx, Workspace* ws, size_t nb, const uint32_t* counts, s
 // Upload per-signature messages, signatures and raw keys to the workspace (uncached-key paths).
 int upload_sig_keys(nw_ctx* ctx, Workspace* ws, const uint8_t* const* msg, const size_t* len,
                     const uint8_t (*pk)[32], const uint8_t (*sig)[64], size_t n, hipStream_t st) {
-    int rc = upload_messages(ctx, ws, msg, len, n, st);
+    const size_t total = message_bytes(len, n);
+    Stager sg(ws, st);
+    NW_TRY(sg.reserve(message_stage_bytes(total, n) + Stager::room(n * 64) + Stager::room(n * 32)), "pinned io");
+    int rc = upload_messages(ctx, ws, sg, msg, len, n, total);
     if (rc != NW_OK) return rc;
     NW_TRY(ws->ensure(ws->w_sig, n * 64 + 64), "ws sig");
     NW_TRY(ws->ensure(ws->w_keys, n * 32 + 32), "ws keys");
-    NW_TRY(hipMemcpyAsync(ws->w_sig.p, sig, n * 64, hipMemcpyHostToDevice, st), "H2D sig");
-    NW_TRY(hipMemcpyAsync(ws->w_keys.p, pk, n * 32, hipMemcpyHostToDevice, st), "H2D keys");
+    NW_TRY(sg.put(ws->w_sig.p, sig, n * 64), "H2D sig");
+    NW_TRY(sg.put(ws->w_keys.p, pk, n * 32), "H2D keys");
     return NW_OK;
 }
 
@@ -698,7 +748,11 @@ int run_generic(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const
             if (rc != NW_OK) return rc;
         }
     } else {
-        rc = upload_messages(ctx, ws, msg, len, n, st);
+        const size_t total = message_bytes(len, n);
+        Stager sg(ws, st);
+        NW_TRY(sg.reserve(message_stage_bytes(total, n) + Stager::room(n * 64) + Stager::room(n * 4) + 512),
+               "pinned io");
+        rc = upload_messages(ctx, ws, sg, msg, len, n, total);
         if (rc != NW_OK) return rc;
         NW_TRY(ws->ensure(ws->w_sig, n * 64), "ws sig");
         NW_TRY(ws->ensure(ws->w_signer, n * 4), "ws signer");
@@ -707,10 +761,10 @@ int run_generic(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const
         NW_TRY(ws->ensure(ws->w_cert_ok, 16), "ws cert_ok");
         NW_TRY(ws->ensure(ws->w_ok, n + 16), "ws ok");
         const uint32_t first = 0, nv = (uint32_t)n;
-        NW_TRY(hipMemcpyAsync(ws->w_sig.p, sig, n * 64, hipMemcpyHostToDevice, st), "H2D sig");
-        NW_TRY(hipMemcpyAsync(ws->w_signer.p, slots.data(), n * 4, hipMemcpyHostToDevice, st), "H2D signer");
-        NW_TRY(hipMemcpyAsync(ws->w_cert_first.p, &first, 4, hipMemcpyHostToDevice, st), "H2D first");
-        NW_TRY(hipMemcpyAsync(ws->w_cert_n.p, &nv, 4, hipMemcpyHostToDevice, st), "H2D n");
+        NW_TRY(sg.put(ws->w_sig.p, sig, n * 64), "H2D sig");
+        NW_TRY(sg.put(ws->w_signer.p, slots.data(), n * 4), "H2D signer");
+        NW_TRY(sg.put(ws->w_cert_first.p, &first, 4), "H2D first");
+        NW_TRY(sg.put(ws->w_cert_n.p, &nv, 4), "H2D n");
         rc = enqueue_certs(ctx, ws, 1, ws->w_cert_first.as<uint32_t>(), ws->w_cert_n.as<uint32_t>(), n,
                            ws->w_sig.as<uint8_t>(), ws->w_signer.as<uint32_t>(), 1, nullptr, ws->w_msg.as<uint8_t>(),
                            ws->w_msg_off.as<uint64_t>(), ws->w_msg_len.as<uint64_t>(), zseed, batch_index, batch_mode,
@@ -1009,7 +1063,10 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
     if (!ws) return NW_ERR_DEVICE;
     hipStream_t st = ws->stream;
     NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
-    // one staged H2D of every input and one D2H of every output (single-certificate latency)
+    // Small calls (single-certificate latency): every input staged into pinned memory, one H2D and
+    // one D2H.  Large calls: the signature and signer arrays go straight from the caller's pageable
+    // buffers (see kDirectCopyBytes).
+    const bool direct = nsigs * 64 >= kDirectCopyBytes;
     const size_t o_sig = 0, o_signer = align256(o_sig + nsigs * 64), o_first = align256(o_signer + nsigs * 4),
                  o_nv = align256(o_first + ncerts * 4), o_msg = align256(o_nv + ncerts * 4),
                  in_bytes = align256(o_msg + ncerts * 32);
@@ -1018,16 +1075,23 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
     NW_TRY(ws->ensure(ws->w_io, in_bytes + out_bytes), "ws io");
     NW_TRY(ws->h_io.ensure(in_bytes > out_bytes ? in_bytes : out_bytes), "pinned io");
     uint8_t* h = ws->h_io.bytes();
-    if (nsigs) {
+    uint8_t* d_in = ws->w_io.as<uint8_t>();
+    uint8_t* d_out = d_in + in_bytes;
+    if (nsigs && !direct) {
         std::memcpy(h + o_sig, sig, nsigs * 64);
         std::memcpy(h + o_signer, signer_slot, nsigs * 4);
     }
     std::memcpy(h + o_first, first.data(), ncerts * 4);
     std::memcpy(h + o_nv, nv.data(), ncerts * 4);
     std::memcpy(h + o_msg, msg, ncerts * 32);
-    uint8_t* d_in = ws->w_io.as<uint8_t>();
-    uint8_t* d_out = d_in + in_bytes;
-    NW_TRY(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, st), "H2D inputs");
+    if (direct) {
+        NW_TRY(hipMemcpyAsync(d_in + o_sig, sig, nsigs * 64, hipMemcpyHostToDevice, st), "H2D sig");
+        NW_TRY(hipMemcpyAsync(d_in + o_signer, signer_slot, nsigs * 4, hipMemcpyHostToDevice, st), "H2D signer");
+        NW_TRY(hipMemcpyAsync(d_in + o_first, h + o_first, in_bytes - o_first, hipMemcpyHostToDevice, st),
+               "H2D inputs");
+    } else {
+        NW_TRY(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, st), "H2D inputs");
+    }
     int rc = enqueue_certs(ctx, ws, ncerts, reinterpret_cast<const uint32_t*>(d_in + o_first),
                            reinterpret_cast<const uint32_t*>(d_in + o_nv), nsigs, d_in + o_sig,
                            reinterpret_cast<const uint32_t*>(d_in + o_signer), 0, d_in + o_msg, nullptr, nullptr,
@@ -1071,7 +1135,12 @@ int nw_verify_batches(nw_ctx* ctx, size_t nb, const uint32_t* first, const uint3
     if (!ws) return NW_ERR_DEVICE;
     hipStream_t st = ws->stream;
     NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
-    int rc = upload_messages(ctx, ws, msg, len, nsigs, st);
+    const size_t total = message_bytes(len, nsigs);
+    Stager sg(ws, st);
+    NW_TRY(sg.reserve(message_stage_bytes(total, nsigs) + Stager::room(nsigs * 64) + Stager::room(nsigs * 4) +
+                      2 * Stager::room(nb * 4)),
+           "pinned io");
+    int rc = upload_messages(ctx, ws, sg, msg, len, nsigs, total);
     if (rc != NW_OK) return rc;
     NW_TRY(ws->ensure(ws->w_sig, nsigs * 64 + 64), "ws sig");
     NW_TRY(ws->ensure(ws->w_signer, nsigs * 4 + 4), "ws signer");
@@ -1079,14 +1148,10 @@ int nw_verify_batches(nw_ctx* ctx, size_t nb, const uint32_t* first, const uint3
     NW_TRY(ws->ensure(ws->w_cert_n, nb * 4 + 4), "ws n");
     NW_TRY(ws->ensure(ws->w_cert_ok, nb + 16), "ws batch_ok");
     NW_TRY(ws->ensure(ws->w_ok, nsigs + 16), "ws ok");
-    if (nsigs) {
-        NW_TRY(hipMemcpyAsync(ws->w_sig.p, sig, nsigs * 64, hipMemcpyHostToDevice, st), "H2D sig");
-        NW_TRY(hipMemcpyAsync(ws->w_signer.p, signer_slot, nsigs * 4, hipMemcpyHostToDevice, st), "H2D signer");
-    }
-    if (nb) {
-        NW_TRY(hipMemcpyAsync(ws->w_cert_first.p, first, nb * 4, hipMemcpyHostToDevice, st), "H2D first");
-        NW_TRY(hipMemcpyAsync(ws->w_cert_n.p, nvotes, nb * 4, hipMemcpyHostToDevice, st), "H2D n");
-    }
+    NW_TRY(sg.put(ws->w_sig.p, sig, nsigs * 64), "H2D sig");
+    NW_TRY(sg.put(ws->w_signer.p, signer_slot, nsigs * 4), "H2D signer");
+    NW_TRY(sg.put(ws->w_cert_first.p, first, nb * 4), "H2D first");
+    NW_TRY(sg.put(ws->w_cert_n.p, nvotes, nb * 4), "H2D n");
     rc = enqueue_certs(ctx, ws, nb, ws->w_cert_first.as<uint32_t>(), ws->w_cert_n.as<uint32_t>(), nsigs,
                        ws->w_sig.as<uint8_t>(), ws->w_signer.as<uint32_t>(), 1, nullptr, ws->w_msg.as<uint8_t>(),
                        ws->w_msg_off.as<uint64_t>(), ws->w_msg_len.as<uint64_t>(), zseed, batch_base, 1,
