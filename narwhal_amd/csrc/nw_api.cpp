@@ -130,7 +130,7 @@ constexpr size_t kMaxWorkspaces = 64;   // one per concurrently calling thread (
 struct nw_ctx {
     int device = 0;
     hipStream_t stream = nullptr;   // administrative stream: basepoint table, committee loads
-    uint32_t finish_k = FINISH_K;   // k_finish signatures per lane
+    uint32_t finish_k = 0;          // k_finish signatures per lane (0: adaptive, finish_k_for)
     // key cache (shared by all calls; guarded by keys_mu)
     std::shared_mutex keys_mu;
     uint32_t* d_btab = nullptr;
@@ -160,6 +160,13 @@ struct nw_ctx {
 };
 
 namespace {
+
+uint32_t finish_k_for(const nw_ctx* ctx, size_t n) {
+    if (ctx->finish_k) return ctx->finish_k;
+    const size_t lanes = 256 * 4 * 64;
+    const size_t k = (n + lanes - 1) / lanes;
+    return k < 1 ? 1u : (k > (size_t)FINISH_K ? (uint32_t)FINISH_K : (uint32_t)k);
+}
 
 // Diagnostics are per calling thread (a context is shared by many threads).
 void set_error(nw_ctx*, const std::string& msg) { tl_last_error = msg; }
@@ -259,14 +266,27 @@ const uint8_t kBaseEnc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x
 // splitting a batch into chunks so k_finish of one chunk overlaps k_verify of the next on a second
 // stream was slower (623 vs 712 M sigs/s at C2: the co-running k_finish waves take VGPR slots from
 // the VALU-bound k_verify and every chunk pays a tail), so a batch is one k_verify + one k_finish.
+// NW_FK = 0 (default): adaptive, see finish_k_for.
 uint32_t finish_k() {
     const char* e = std::getenv("NW_FK");
     const long k = e ? std::strtol(e, nullptr, 10) : 0;
-    return k >= 1 && k <= FINISH_K ? (uint32_t)k : (uint32_t)FINISH_K;
+    return k >= 1 && k <= FINISH_K ? (uint32_t)k : 0u;
 }
 
+// Signatures per k_finish lane for a launch of n: just enough that the lanes fit one wave per SIMD
+// (256 CUs x 4 SIMDs x 64 lanes), because below that the kernel is bound by the serial
+// prefix-product chain + inversion of each lane, not by the inversion count.  A single
+// certificate (67 .. 6,667 signatures) gets one signature per lane: one inversion per signature,
+// no chain; C2's million signatures get 16 per lane.
+uint32_t finish_k_for(const nw_ctx* ctx, size_t n);
+
 constexpr size_t KEY_CACHE_BUDGET = 160ull << 30;  // bytes of HBM for key tables by default (of 288 GB)
-constexpr size_t kGroupMinSigs = 16384;            // group signatures by signer above this batch size
+// Group signatures by signer (key-table locality) above this batch size, and only when keys repeat
+// (at least kGroupMinSigsPerKey signatures per cached key on average): the worker's load (62,500
+// signatures over 100,000 keys, each key at most once) gains nothing from the order and would pay
+// the 100,000-slot scan (0.16 ms of a 0.47 ms batch, profiles/r02/kernel_stats_w_r02.csv).
+constexpr size_t kGroupMinSigs = 16384;
+constexpr size_t kGroupMinSigsPerKey = 4;
 
 // Key comb window, fixed at the first load.  Auto (0): a conservative choice that leaves room for
 // keys added later.  Committee mode (-1): the first load IS the committee; take the widest window
@@ -419,7 +439,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
                   size_t nsigs, const uint8_t* d_sig, const uint32_t* d_signer, int msgmode, const uint8_t* d_msg32,
                   const uint8_t* d_msg_base, const uint64_t* d_msg_off, const uint64_t* d_msg_len,
                   const uint8_t* zseed, uint64_t cert_base, uint32_t batch_mode, uint8_t* d_cert_ok,
-                  uint32_t* d_flags_user, uint64_t* d_stake_out, hipStream_t st) {
+                  uint32_t* d_flags_user, uint64_t* d_stake_out, hipStream_t st, uint8_t* d_sig_ok = nullptr) {
     uint32_t* d_flags = d_flags_user;
     if (!d_flags) {
         NW_TRY(ws->ensure(ws->w_flags, nsigs * 4 + 4), "ws flags");
@@ -465,7 +485,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     vp.pbuf = ws->w_pbuf.as<uint32_t>();
     vp.pre = ws->w_pre.as<uint32_t>();
     vp.perm = nullptr;
-    if (nsigs >= kGroupMinSigs && ctx->nkeys > 1) {
+    if (nsigs >= kGroupMinSigs && ctx->nkeys > 1 && nsigs >= kGroupMinSigsPerKey * ctx->nkeys) {
         NW_TRY(ws->ensure(ws->w_counts, ctx->nkeys * 4 + 16), "ws counts");
         NW_TRY(ws->ensure(ws->w_cursor, ctx->nkeys * 4 + 16), "ws cursor");
         NW_TRY(ws->ensure(ws->w_perm, nsigs * 4 + 16), "ws perm");
@@ -476,7 +496,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     }
     vp.g0 = 0;
     vp.gn = (uint32_t)nsigs;
-    vp.fk = ctx->finish_k;
+    vp.fk = finish_k_for(ctx, nsigs);
     hipEvent_t ev_stop = nullptr;
     {
         std::lock_guard<std::mutex> g(ctx->prof_mu);
@@ -496,7 +516,10 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     NW_TRY(launch_verify(vp, msgmode, ctx->key_window, st), "k_verify");
     if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");   // brackets k_verify alone
     NW_TRY(launch_finish(vp, st), "k_finish");
-    if (!batch_mode) return NW_OK;
+    if (!batch_mode) {   // strict verdicts only: no certificate pass
+        if (d_sig_ok) NW_TRY(launch_flags_to_ok((uint32_t)nsigs, d_flags, d_sig_ok, st), "k_flags_to_ok");
+        return NW_OK;
+    }
 
     NW_TRY(launch_slow(vp, msgmode, ctx->key_window, (uint32_t)nsigs, st), "k_slow_sig");
 
@@ -512,6 +535,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     fp.slow_buf = vp.slow_buf;
     fp.cert_ok = d_cert_ok;
     fp.accepted_stake = d_stake_out;
+    fp.sig_ok = d_sig_ok;
     NW_TRY(launch_finalize(fp, st), "k_cert_finalize");
     return NW_OK;
 }
@@ -570,12 +594,21 @@ int upload_messages(nw_ctx* ctx, Workspace* ws, Stager& sg, const uint8_t* const
     uint8_t* packed = sg.alloc(total + 8);
     uint64_t* off = reinterpret_cast<uint64_t*>(sg.alloc(n * 8 + 8));
     uint64_t* ln = reinterpret_cast<uint64_t*>(sg.alloc(n * 8 + 8));
+    // messages laid out back to back in the caller's memory (the worker's fixed 8-byte messages,
+    // numpy rows) are copied as one block instead of one memcpy each
+    bool contiguous = n > 0;
     size_t pos = 0;
     for (size_t i = 0; i < n; ++i) {
         off[i] = pos;
         ln[i] = len[i];
-        if (len[i]) std::memcpy(packed + pos, msg[i], len[i]);
+        contiguous = contiguous && msg[i] == msg[0] + pos;
         pos += len[i];
+    }
+    if (contiguous) {
+        if (pos) std::memcpy(packed, msg[0], pos);
+    } else {
+        for (size_t i = 0; i < n; ++i)
+            if (len[i]) std::memcpy(packed + off[i], msg[i], len[i]);
     }
     std::memset(packed + pos, 0, 8);
     NW_TRY(sg.copy(ws->w_msg.p, packed, total + 8), "H2D msg");
@@ -597,7 +630,7 @@ int enqueue_strict_var(nw_ctx* ctx, Workspace* ws, size_t n, hipStream_t st) {
     vp.n = (uint32_t)n;
     vp.g0 = 0;
     vp.gn = (uint32_t)n;
-    vp.fk = ctx->finish_k;
+    vp.fk = finish_k_for(ctx, n);
     vp.batch_mode = 0;
     vp.sig = ws->w_sig.as<uint8_t>();
     vp.sig_keys = ws->w_keys.as<uint32_t>();
@@ -768,12 +801,14 @@ int run_generic(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const
         rc = enqueue_certs(ctx, ws, 1, ws->w_cert_first.as<uint32_t>(), ws->w_cert_n.as<uint32_t>(), n,
                            ws->w_sig.as<uint8_t>(), ws->w_signer.as<uint32_t>(), 1, nullptr, ws->w_msg.as<uint8_t>(),
                            ws->w_msg_off.as<uint64_t>(), ws->w_msg_len.as<uint64_t>(), zseed, batch_index, batch_mode,
-                           ws->w_cert_ok.as<uint8_t>(), nullptr, nullptr, st);
+                           ws->w_cert_ok.as<uint8_t>(), nullptr, nullptr, st,
+                           ok_out ? ws->w_ok.as<uint8_t>() : nullptr);   // verdict bytes from k_cert_finalize
         if (rc != NW_OK) return rc;
     }
     if (ok_out) {
-        NW_TRY(launch_flags_to_ok((uint32_t)n, ws->w_flags.as<uint32_t>(), ws->w_ok.as<uint8_t>(), st),
-               "k_flags_to_ok");
+        if (!cached)
+            NW_TRY(launch_flags_to_ok((uint32_t)n, ws->w_flags.as<uint32_t>(), ws->w_ok.as<uint8_t>(), st),
+                   "k_flags_to_ok");
         NW_TRY(hipMemcpyAsync(ok_out, ws->w_ok.p, n, hipMemcpyDeviceToHost, st), "D2H ok");
     }
     if (verdict_out) NW_TRY(hipMemcpyAsync(verdict_out, ws->w_cert_ok.p, 1, hipMemcpyDeviceToHost, st), "D2H");
@@ -1096,10 +1131,8 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
                            reinterpret_cast<const uint32_t*>(d_in + o_nv), nsigs, d_in + o_sig,
                            reinterpret_cast<const uint32_t*>(d_in + o_signer), 0, d_in + o_msg, nullptr, nullptr,
                            nullptr, zseed, cert_base, 1, d_out + o_cok, nullptr,
-                           reinterpret_cast<uint64_t*>(d_out + o_stake), st);
+                           reinterpret_cast<uint64_t*>(d_out + o_stake), st, sig_ok && nsigs ? d_out + o_ok : nullptr);
     if (rc != NW_OK) return rc;   // the lease synchronizes the stream (the H2D may be in flight)
-    if (sig_ok && nsigs)
-        NW_TRY(launch_flags_to_ok((uint32_t)nsigs, ws->w_flags.as<uint32_t>(), d_out + o_ok, st), "k_flags_to_ok");
     // the H2D above has completed in stream order before this copy overwrites the staging buffer
     NW_TRY(hipMemcpyAsync(h, d_out, out_bytes, hipMemcpyDeviceToHost, st), "D2H outputs");
     NW_TRY(hipStreamSynchronize(st), "sync");
@@ -1155,13 +1188,10 @@ int nw_verify_batches(nw_ctx* ctx, size_t nb, const uint32_t* first, const uint3
     rc = enqueue_certs(ctx, ws, nb, ws->w_cert_first.as<uint32_t>(), ws->w_cert_n.as<uint32_t>(), nsigs,
                        ws->w_sig.as<uint8_t>(), ws->w_signer.as<uint32_t>(), 1, nullptr, ws->w_msg.as<uint8_t>(),
                        ws->w_msg_off.as<uint64_t>(), ws->w_msg_len.as<uint64_t>(), zseed, batch_base, 1,
-                       ws->w_cert_ok.as<uint8_t>(), nullptr, nullptr, st);
+                       ws->w_cert_ok.as<uint8_t>(), nullptr, nullptr, st,
+                       sig_ok && nsigs ? ws->w_ok.as<uint8_t>() : nullptr);
     if (rc != NW_OK) return rc;
-    if (sig_ok && nsigs) {
-        NW_TRY(launch_flags_to_ok((uint32_t)nsigs, ws->w_flags.as<uint32_t>(), ws->w_ok.as<uint8_t>(), st),
-               "k_flags_to_ok");
-        NW_TRY(hipMemcpyAsync(sig_ok, ws->w_ok.p, nsigs, hipMemcpyDeviceToHost, st), "D2H sig_ok");
-    }
+    if (sig_ok && nsigs) NW_TRY(hipMemcpyAsync(sig_ok, ws->w_ok.p, nsigs, hipMemcpyDeviceToHost, st), "D2H sig_ok");
     if (batch_ok && nb) NW_TRY(hipMemcpyAsync(batch_ok, ws->w_cert_ok.p, nb, hipMemcpyDeviceToHost, st), "D2H");
     NW_TRY(hipStreamSynchronize(st), "sync");
     lease.synced();

@@ -153,8 +153,47 @@ NW_HD uint32_t dbl32(uint32_t x) {
 #endif
 }
 
+// Product scanning with the carry fused into the next column (NW_FUSED_CARRY, experimental):
+// column k's multiply-accumulate chain starts from the carry out of column k-1, so the carry
+// needs no separate 64-bit add; the wrap carry (x19) and one 0 -> 1 carry tighten the result.
+// Same bounds as fe_reduce_wide (limb 1 <= 2^25 + 2^18).
+#ifndef NW_FUSED_CARRY
+#define NW_FUSED_CARRY 0
+#endif
+NW_HD fe fe_fused_wrap(uint32_t r[10], uint64_t c) {
+    const uint64_t t = (uint64_t)r[0] + c * 19u;
+    r[0] = (uint32_t)t & M26;
+    r[1] += (uint32_t)(t >> 26);
+    fe o;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) o.v[i] = r[i];
+    return o;
+}
+
 // h = f * g mod p.  Coefficient of f_i g_j: 2 if i, j both odd; x19 if i + j >= 10.
 NW_HD fe fe_mul(const fe& f, const fe& g) {
+#if NW_FUSED_CARRY
+    uint32_t g19[10], f2[10], r[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) g19[j] = 19u * g.v[j];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) f2[i] = (i & 1) ? dbl32(f.v[i]) : f.v[i];
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        uint64_t acc = c;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            const int j = (k - i + 10) % 10;
+            const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
+            const uint32_t b = (i + j >= 10) ? g19[j] : g.v[j];
+            acc += (uint64_t)a * b;
+        }
+        r[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
+        c = acc >> ((k & 1) ? 25 : 26);
+    }
+    return fe_fused_wrap(r, c);
+#else
     uint32_t g19[10];
 #pragma unroll
     for (int j = 0; j < 10; ++j) g19[j] = 19u * g.v[j];
@@ -174,10 +213,32 @@ NW_HD fe fe_mul(const fe& f, const fe& g) {
         }
     }
     return fe_reduce_wide(acc);
+#endif
 }
 
 // h = f^2 mod p (55 products).
 NW_HD fe fe_sq(const fe& f) {
+#if NW_FUSED_CARRY
+    uint32_t r[10];
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        uint64_t acc = c;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            const int j = (k - i + 10) % 10;
+            if (j < i) continue;   // each unordered pair once
+            uint32_t m1 = (i == j) ? 1u : 2u;
+            if ((i & 1) && (j & 1)) m1 *= 2u;
+            const uint32_t a = f.v[i] * m1;
+            const uint32_t b = (i + j >= 10) ? 19u * f.v[j] : f.v[j];
+            acc += (uint64_t)a * b;
+        }
+        r[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
+        c = acc >> ((k & 1) ? 25 : 26);
+    }
+    return fe_fused_wrap(r, c);
+#else
     uint64_t acc[10];
 #pragma unroll
     for (int k = 0; k < 10; ++k) acc[k] = 0;
@@ -193,6 +254,7 @@ NW_HD fe fe_sq(const fe& f) {
         }
     }
     return fe_reduce_wide(acc);
+#endif
 }
 
 NW_HD fe fe_sqn(fe f, int n) {

@@ -138,6 +138,116 @@ NW_HD void s30_normalize(s30& r, int32_t sgn) {
     }
 }
 
+// Variable-time divsteps (Bernstein-Yang as restated in Wuille's "safegcd implementation" notes,
+// with eta = -delta, delta starting at 1): runs of zeros in g are consumed at once, and each odd
+// g is combined with f using a multiplier w that clears min(eta + 1, remaining, 4 or 6) low bits.
+// The inputs are public (verification), so variable time is acceptable; the lanes of a wave
+// diverge in the iteration count, which costs the maximum over the wave, still well below the 30
+// fixed branch-free steps.  Same transition-matrix contract as s30_divsteps.
+NW_HD int32_t s30_divsteps_var(int32_t eta, uint32_t f, uint32_t g, s30_trans& t) {
+    uint32_t u = 1, v = 0, q = 0, r = 1;
+    int i = 30;
+    for (;;) {
+        // sentinel bit at position i: count zeros only up to the remaining steps
+        const int zeros = __builtin_ctz(g | (0xFFFFFFFFu << i));
+        g >>= zeros;
+        u <<= zeros;
+        v <<= zeros;
+        eta -= zeros;
+        i -= zeros;
+        if (i == 0) break;
+        uint32_t w, m;
+        int limit;
+        if (eta < 0) {
+            eta = -eta;
+            uint32_t tmp = f;
+            f = g;
+            g = 0u - tmp;
+            tmp = u;
+            u = q;
+            q = 0u - tmp;
+            tmp = v;
+            v = r;
+            r = 0u - tmp;
+            limit = (eta + 1) > i ? i : (eta + 1);
+            m = (0xFFFFFFFFu >> (32 - limit)) & 63u;
+            w = (f * g * (f * f - 2u)) & m;   // -g / f mod 2^6
+        } else {
+            limit = (eta + 1) > i ? i : (eta + 1);
+            m = (0xFFFFFFFFu >> (32 - limit)) & 15u;
+            w = f + (((f + 1u) & 4u) << 1);   // f^-1 mod 2^4
+            w = (0u - w * g) & m;
+        }
+        g += f * w;
+        q += u * w;
+        r += v * w;
+    }
+    t.u = (int32_t)u;
+    t.v = (int32_t)v;
+    t.q = (int32_t)q;
+    t.r = (int32_t)r;
+    return eta;
+}
+
+NW_HD bool s30_is_zero(const s30& a) {
+    int32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) o |= a.v[i];
+    return o == 0;
+}
+
+NW_HD void fe_to_s30(s30& g, const fe& z) {
+    uint32_t w[8];
+    fe_tobytes_w(w, z);
+    g.v[0] = (int32_t)(w[0] & S30_M);
+    g.v[1] = (int32_t)(((w[0] >> 30) | (w[1] << 2)) & S30_M);
+    g.v[2] = (int32_t)(((w[1] >> 28) | (w[2] << 4)) & S30_M);
+    g.v[3] = (int32_t)(((w[2] >> 26) | (w[3] << 6)) & S30_M);
+    g.v[4] = (int32_t)(((w[3] >> 24) | (w[4] << 8)) & S30_M);
+    g.v[5] = (int32_t)(((w[4] >> 22) | (w[5] << 10)) & S30_M);
+    g.v[6] = (int32_t)(((w[5] >> 20) | (w[6] << 12)) & S30_M);
+    g.v[7] = (int32_t)(((w[6] >> 18) | (w[7] << 14)) & S30_M);
+    g.v[8] = (int32_t)(w[7] >> 16);
+}
+
+// [0, p) in 30-bit limbs -> radix 2^25.5
+NW_HD fe s30_to_fe(const s30& d) {
+    uint32_t w[8];
+    w[0] = (uint32_t)d.v[0] | ((uint32_t)d.v[1] << 30);
+    w[1] = ((uint32_t)d.v[1] >> 2) | ((uint32_t)d.v[2] << 28);
+    w[2] = ((uint32_t)d.v[2] >> 4) | ((uint32_t)d.v[3] << 26);
+    w[3] = ((uint32_t)d.v[3] >> 6) | ((uint32_t)d.v[4] << 24);
+    w[4] = ((uint32_t)d.v[4] >> 8) | ((uint32_t)d.v[5] << 22);
+    w[5] = ((uint32_t)d.v[5] >> 10) | ((uint32_t)d.v[6] << 20);
+    w[6] = ((uint32_t)d.v[6] >> 12) | ((uint32_t)d.v[7] << 18);
+    w[7] = ((uint32_t)d.v[7] >> 14) | ((uint32_t)d.v[8] << 16);
+    return fe_frombytes_w(w);
+}
+
+// z^-1 mod p (0 -> 0) in variable time: batches of 30 variable-time divsteps until g = 0 (for
+// every lane of the wave: the loop condition is per lane, finished lanes idle).
+NW_HD fe fe_invert_var(const fe& z) {
+    s30 f, g, d, e;
+    fe_to_s30(g, z);
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+        f.v[i] = S30_P[i];
+        d.v[i] = 0;
+        e.v[i] = 0;
+    }
+    e.v[0] = 1;
+    int32_t eta = -1;
+#pragma nounroll
+    for (int it = 0; it < 40 && !s30_is_zero(g); ++it) {
+        s30_trans t;
+        eta = s30_divsteps_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+        s30_update_de(d, e, t);
+        s30_update_fg(f, g, t);
+    }
+    s30_normalize(d, f.v[8]);
+    return s30_to_fe(d);
+}
+
 // z^-1 mod p (0 -> 0), same result as fe_invert.
 NW_HD fe fe_invert_sg(const fe& z) {
     uint32_t w[8];

@@ -63,6 +63,7 @@ struct FinalizeParams {
     const uint32_t* slow_buf;
     uint8_t* cert_ok;              // [ncerts] (may be null)
     uint64_t* accepted_stake;      // [ncerts] (may be null)
+    uint8_t* sig_ok;               // [nsigs] strict verdict bytes (may be null; k_flags_to_ok fused)
 };
 
 hipError_t launch_verify(const VerifyParams& p, int msgmode, int key_window, hipStream_t st);

@@ -119,6 +119,9 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
 }
 
 // ------------------------------------------------------------------------------------ finish
+#ifndef NW_INV_VAR
+#define NW_INV_VAR 1
+#endif
 // Montgomery batch inversion of the Z of FINISH_K signatures per lane (one field inversion per
 // chunk), affine x, y, encoding match against R, strict verdict, and (batch mode) compaction of the
 // mismatching signatures into the exact-path list.  Lane L of NL owns the processing-order columns
@@ -143,7 +146,14 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
             store_fe_soa(a.pre, n, g, acc);
         }
     }
-    fe inv = fe_invert_sg(acc);
+    // Inversion: variable-time safegcd (public data) when each lane chains several signatures
+    // (throughput-bound launches: fewer instructions on average); the branch-free constant-time
+    // divsteps for one signature per lane (latency-bound launches: with 64 independent inversions
+    // per wave the variable-time loop runs the slowest lane's count, measured 10% slower there:
+    // profiles/r02/ab_r02.txt).  a.fk is uniform, so the branch does not diverge.
+    fe inv;
+    if (NW_INV_VAR && a.fk >= 4) inv = fe_invert_var(acc);
+    else inv = fe_invert_sg(acc);
 #pragma unroll
     for (int k = FINISH_K - 1; k >= 0; --k) {
         if ((uint32_t)k < cnt) {
@@ -173,6 +183,11 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
 __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (a.sig_ok) {   // strict verdict bytes of every signature (the flags are final here)
+        const uint32_t nthr = gridDim.x * blockDim.x;
+        for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < a.nsigs; v += nthr)
+            a.sig_ok[v] = (a.flags[v] & NW_F_STRICT) ? 1 : 0;
+    }
     if (c >= a.ncerts) return;   // whole wave exits together
     const uint32_t first = a.cert_first[c];
     // a vote range past the signature array (device inputs are not host-checked) rejects the

@@ -80,6 +80,11 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     store_prec_soa(a.pbuf, a.n, gid, P, verify_pflags(P, R, frow[gid]));
 }
 
+// Latency-mode kernel for small launches (nw_verify_split.h, compiled in nw_kvs.hip).
+static constexpr uint32_t VERIFY_SPLIT_MAX_SIGS = 16384;
+template <int WA>
+hipError_t launch_split_wa(const VerifyParams& p, int msgmode, hipStream_t st);
+
 // Exact path for signatures with D_i != O: Q_i = z_i (R_i - P_i); R decode failure -> F_R_BAD.
 template <int MSGMODE, int WA>
 __global__ void __launch_bounds__(256) k_slow_sig(VerifyParams a) {
@@ -106,6 +111,7 @@ template <int WA>
 hipError_t launch_vs_wa(const VerifyParams& p, int msgmode, bool slow, uint32_t n_upper, hipStream_t st) {
     const dim3 b(256);
     const dim3 g(blocks_for(slow ? n_upper : p.gn, 256));
+    if (!slow && p.gn <= VERIFY_SPLIT_MAX_SIGS) return launch_split_wa<WA>(p, msgmode, st);
     if (msgmode == 0) {
         if (slow) hipLaunchKernelGGL((k_slow_sig<0, WA>), g, b, 0, st, p);
         else hipLaunchKernelGGL((k_verify<0, WA>), g, b, 0, st, p);

@@ -1,0 +1,139 @@
+// Latency-mode k_verify (k_verify_split) for small launches; compiled once per key window in
+// nw_kvs.hip (a separate object from nw_kv.hip so the two heavy halves build in parallel).
+#pragma once
+#include "nw_verify_kernels.h"
+
+namespace nw {
+
+// ------------------------------------------------------------------------------------ latency mode
+// Small launches (a single certificate, a vote batch: fewer signatures than the chip has SIMD
+// lanes / VERIFY_SPLIT) leave most SIMDs idle and run each wave alone, at the lone-wave issue rate,
+// so k_verify's time is the length of ONE signature's comb chain.  Here VERIFY_SPLIT lanes share a
+// signature: the NPOS = comb_pos(WB) + comb_pos(WA) positions of its two combs are cut into
+// contiguous blocks, each lane sums its block, and two shuffle levels add the partial points.
+// Digits are taken from k' = k + sum_p 2^(W-1) 2^(W p) (signed radix-2^W digit p = window p of k'
+// minus 2^(W-1)), so any lane can start at any position without the serial carry chain.  The
+// output record is the one k_verify writes, for the same k_finish.
+static constexpr int VERIFY_SPLIT = 4;
+// VERIFY_SPLIT_MAX_SIGS (nw_verify_kernels.h): the split grid is then <= one wave per SIMD
+// (1,024 SIMDs x 64 lanes / VERIFY_SPLIT)
+static_assert(VERIFY_SPLIT_MAX_SIGS * VERIFY_SPLIT <= 256 * 4 * 64, "split grid larger than one wave per SIMD");
+
+// k + sum_{p < comb_pos(W)} 2^(W-1) 2^(W p) for k < 2^253 (< 2^(W comb_pos(W)) for every window).
+template <int W>
+NW_HD void offset_scalar(uint32_t kp[9], const uint32_t k[8]) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int w = 0; w < 9; ++w) {
+        uint32_t add = 0;
+#pragma unroll
+        for (int p = 0; p < comb_pos(W); ++p) {
+            const int bit = W * p + W - 1;
+            if ((bit >> 5) == w) add |= 1u << (bit & 31);
+        }
+        c += (uint64_t)(w < 8 ? k[w] : 0u) + add;
+        kp[w] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+
+template <int W>
+NW_HD void shift_window(uint32_t kp[9]) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) kp[w] = (kp[w] >> W) | (kp[w + 1] << (32 - W));
+    kp[8] >>= W;
+}
+
+template <int W>
+NW_HD int low_digit(const uint32_t kp[9]) {
+    return (int)(kp[0] & ((1u << W) - 1u)) - (1 << (W - 1));
+}
+
+template <int MSGMODE, int WA>
+__global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
+    constexpr int WB = B_WINDOW;
+    constexpr int PB = comb_pos(WB), NPOS = PB + comb_pos(WA);
+    constexpr int K = (NPOS + VERIFY_SPLIT - 1) / VERIFY_SPLIT;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t j = t % VERIFY_SPLIT;
+    // whole signature groups exit together (VERIFY_SPLIT divides 64): the shuffles below see
+    // only active partners
+    if (t / VERIFY_SPLIT >= a.gn) return;
+    const uint32_t gid = a.g0 + t / VERIFY_SPLIT;
+    const uint32_t i = a.perm ? a.perm[gid] : gid;
+    uint32_t R[8], S[8], h[8], slot, kinfo, cert;
+    lane_inputs<MSGMODE>(a, i, R, S, slot, kinfo, cert, h);
+    const bool sok = sc_is_canonical(S);
+    const bool aok = (kinfo & KI_OK) != 0;
+    uint32_t flags = (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | ((kinfo & KI_SMALL) ? NW_F_A_SMALL : 0u);
+    const uint32_t tk = (kinfo >> KI_TORSION_SHIFT) & 7u;
+    if (a.batch_mode && tk != 0 && sok && aok) {
+        uint32_t z4[4];
+        coeff_z(a, i, cert, z4);
+        flags |= torsion_coef(z4, h, tk) << NW_F_TCOEF_SHIFT;
+    }
+    uint32_t sw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sw[k] = sok ? S[k] : 0u;
+    uint32_t sp[9], hp[9];
+    offset_scalar<WB>(sp, sw);
+    offset_scalar<WA>(hp, h);
+    // advance both recoders to this lane's first position (lane-dependent, cheap shifts)
+    const int p0 = (int)j * K;
+    for (int q = 0; q < p0 && q < PB; ++q) shift_window<WB>(sp);
+    for (int q = PB; q < p0; ++q) shift_window<WA>(hp);
+    const uint32_t* atab = a.key_tab + (size_t)slot * comb_words(WA);
+    ge_p3 P;
+#pragma unroll 1
+    for (int st = 0; st < K; ++st) {
+        const int pos = p0 + st;
+        const bool base = pos < PB;
+        const int db = low_digit<WB>(sp), dk = low_digit<WA>(hp);
+        const int d = base ? db : dk;
+        const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+        // past the last position: entry 0 of base position 0 (the identity), a no-op addition
+        const uint32_t* e = pos >= NPOS ? a.btab
+                            : base      ? a.btab + ((size_t)pos * comb_ent(WB) + ad) * PRECOMP_WORDS
+                                        : atab + ((size_t)(pos - PB) * comb_ent(WA) + ad) * PRECOMP_WORDS;
+        const uint4* q = reinterpret_cast<const uint4*>(e);
+        uint32_t w[32];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint4 v = q[k];
+            w[4 * k] = v.x;
+            w[4 * k + 1] = v.y;
+            w[4 * k + 2] = v.z;
+            w[4 * k + 3] = v.w;
+        }
+        const bool neg = pos < NPOS && (base ? d < 0 : d > 0);
+        const ge_precomp ent = ge_precomp_cneg(ge_precomp_from_words(w), neg);
+        if (st == 0) P = ge_from_precomp(ent);
+        else P = ge_madd(P, ent);
+        if (base) shift_window<WB>(sp);
+        else shift_window<WA>(hp);
+    }
+#pragma unroll
+    for (int off = 1; off < VERIFY_SPLIT; off <<= 1) {
+        ge_p3 o;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) {
+            o.X.v[k] = __shfl_xor(P.X.v[k], off, 64);
+            o.Y.v[k] = __shfl_xor(P.Y.v[k], off, 64);
+            o.Z.v[k] = __shfl_xor(P.Z.v[k], off, 64);
+            o.T.v[k] = __shfl_xor(P.T.v[k], off, 64);
+        }
+        P = ge_add(P, ge_to_cached(o));
+    }
+    if (j != 0) return;
+    store_prec_soa(a.pbuf, a.n, gid, P, verify_pflags(P, R, flags));
+}
+
+template <int WA>
+hipError_t launch_split_wa(const VerifyParams& p, int msgmode, hipStream_t st) {
+    const dim3 b(256), g(blocks_for((uint64_t)p.gn * VERIFY_SPLIT, 256));
+    if (msgmode == 0) hipLaunchKernelGGL((k_verify_split<0, WA>), g, b, 0, st, p);
+    else hipLaunchKernelGGL((k_verify_split<1, WA>), g, b, 0, st, p);
+    return hipGetLastError();
+}
+
+}  // namespace nw

@@ -45,6 +45,7 @@ void hc_fe_mul(const uint8_t* a, const uint8_t* b, uint8_t* out) { fe_out(out, f
 void hc_fe_sq(const uint8_t* a, uint8_t* out) { fe_out(out, fe_sq(fe_in(a))); }
 void hc_fe_invert(const uint8_t* a, uint8_t* out) { fe_out(out, fe_invert(fe_in(a))); }
 void hc_fe_invert_sg(const uint8_t* a, uint8_t* out) { fe_out(out, fe_invert_sg(fe_in(a))); }
+void hc_fe_invert_var(const uint8_t* a, uint8_t* out) { fe_out(out, fe_invert_var(fe_in(a))); }
 void hc_fe_add_sub(const uint8_t* a, const uint8_t* b, uint8_t* sum, uint8_t* diff) {
     const fe fa = fe_in(a), fb = fe_in(b);
     fe_out(sum, fe_add(fa, fb));
