@@ -131,6 +131,7 @@ struct nw_ctx {
     int device = 0;
     hipStream_t stream = nullptr;   // administrative stream: basepoint table, committee loads
     uint32_t finish_k = 0;          // k_finish signatures per lane (0: adaptive, finish_k_for)
+    bool group_off = false;         // NW_GROUP=0: never sort signatures by signer (A/B knob)
     // key cache (shared by all calls; guarded by keys_mu)
     std::shared_mutex keys_mu;
     uint32_t* d_btab = nullptr;
@@ -485,7 +486,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     vp.pbuf = ws->w_pbuf.as<uint32_t>();
     vp.pre = ws->w_pre.as<uint32_t>();
     vp.perm = nullptr;
-    if (nsigs >= kGroupMinSigs && ctx->nkeys > 1 && nsigs >= kGroupMinSigsPerKey * ctx->nkeys) {
+    if (!ctx->group_off && nsigs >= kGroupMinSigs && ctx->nkeys > 1 && nsigs >= kGroupMinSigsPerKey * ctx->nkeys) {
         NW_TRY(ws->ensure(ws->w_counts, ctx->nkeys * 4 + 16), "ws counts");
         NW_TRY(ws->ensure(ws->w_cursor, ctx->nkeys * 4 + 16), "ws cursor");
         NW_TRY(ws->ensure(ws->w_perm, nsigs * 4 + 16), "ws perm");
@@ -844,6 +845,10 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     nw_ctx* ctx = new nw_ctx();
     ctx->device = dev;
     ctx->finish_k = finish_k();
+    {
+        const char* g = std::getenv("NW_GROUP");
+        ctx->group_off = g && g[0] == '0';
+    }
     if (opts && opts->max_keys) {
         ctx->max_keys = opts->max_keys;
         ctx->max_keys_user = true;

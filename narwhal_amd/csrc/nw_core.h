@@ -122,74 +122,75 @@ NW_HD void hram_generic(uint32_t out[16], const uint32_t R[8], const uint32_t A[
     sha512_digest_le32(out, st);
 }
 
+// A table entry as gathered: the 30 payload words of its 128-B line (seven 16-B loads and one 8-B
+// load: the two pad words are never fetched into registers).
+struct ent30 {
+    uint4 q[7];
+    uint2 t;
+};
+
+NW_HD ent30 load_ent30(const uint32_t* __restrict__ p) {
+    ent30 e;
+    const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) e.q[k] = q[k];
+    e.t = reinterpret_cast<const uint2*>(p)[14];
+    return e;
+}
+
+NW_HD ge_precomp ent30_precomp(const ent30& e) {
+    uint32_t w[32];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+        w[4 * k] = e.q[k].x;
+        w[4 * k + 1] = e.q[k].y;
+        w[4 * k + 2] = e.q[k].z;
+        w[4 * k + 3] = e.q[k].w;
+    }
+    w[28] = e.t.x;
+    w[29] = e.t.y;
+    w[30] = 0;
+    w[31] = 0;
+    return ge_precomp_from_words(w);
+}
+
 // One comb pass: P += sum_pos sign(d_pos) * T[pos][|d_pos|] for the signed radix-2^W digits of
 // sc (consumed).  Software-pipelined: the gather of position pos+1's entry is issued before the
-// mixed addition of position pos, so the (HBM) latency hides under ~1.3k VALU instructions of
+// mixed addition of position pos, so the (HBM) latency hides under ~1.1k VALU instructions of
 // field arithmetic.  neg_pos: negate entries for positive digits (-h A).  FIRST: P is the identity
 // on entry, so position 0's entry becomes P directly (ge_from_precomp: 1 multiplication, not 7).
+// (Measured and rejected: two positions per iteration with two alternating buffers, to drop the
+// buffer copy: it spills at the 168-VGPR bound.)
 template <int W, bool FIRST>
 NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab, bool neg_pos) {
     int carry = 0;
     int d = next_digit<W>(sc, carry);
-    const uint4* q = reinterpret_cast<const uint4*>(tab + (size_t)(d < 0 ? -d : d) * PRECOMP_WORDS);
-    uint4 cur[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) cur[k] = q[k];
+    ent30 cur = load_ent30(tab + (size_t)(d < 0 ? -d : d) * PRECOMP_WORDS);
     int pos = 0;
     if constexpr (FIRST) {
         // position 0 starts the chain: P = T[0][|d|] (sign applied), no addition
-        uint32_t w[32];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            w[4 * k] = cur[k].x;
-            w[4 * k + 1] = cur[k].y;
-            w[4 * k + 2] = cur[k].z;
-            w[4 * k + 3] = cur[k].w;
-        }
+        const ge_precomp q0 = ent30_precomp(cur);
         const bool neg0 = neg_pos ? d > 0 : d < 0;
         d = next_digit<W>(sc, carry);   // position 1's digit; its gather overlaps the conversion
-        const uint4* qn = reinterpret_cast<const uint4*>(tab + ((size_t)comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) cur[k] = qn[k];
-        P = ge_from_precomp(ge_precomp_cneg(ge_precomp_from_words(w), neg0));
+        cur = load_ent30(tab + ((size_t)comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
+        P = ge_from_precomp(ge_precomp_cneg(q0, neg0));
         pos = 1;
     }
 #pragma nounroll
     for (; pos < comb_pos(W); ++pos) {
+        int dn = 0;
 #ifdef NW_NO_PREFETCH
-        uint4 nxt[8];
-        int dn = 0;
-        uint32_t w[32];
-        {
-            const uint4* qc = reinterpret_cast<const uint4*>(
-                tab + ((size_t)pos * comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) cur[k] = qc[k];
-        }
+        cur = load_ent30(tab + ((size_t)pos * comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
         if (pos + 1 < comb_pos(W)) dn = next_digit<W>(sc, carry);
+        P = ge_madd(P, ge_precomp_cneg(ent30_precomp(cur), neg_pos ? d > 0 : d < 0));
 #else
-        uint4 nxt[8];
-        int dn = 0;
+        ent30 nxt;
         if (pos + 1 < comb_pos(W)) {
             dn = next_digit<W>(sc, carry);
-            const uint4* qn = reinterpret_cast<const uint4*>(
-                tab + ((size_t)(pos + 1) * comb_ent(W) + (dn < 0 ? -dn : dn)) * PRECOMP_WORDS);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) nxt[k] = qn[k];
+            nxt = load_ent30(tab + ((size_t)(pos + 1) * comb_ent(W) + (dn < 0 ? -dn : dn)) * PRECOMP_WORDS);
         }
-        uint32_t w[32];
-#endif
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            w[4 * k] = cur[k].x;
-            w[4 * k + 1] = cur[k].y;
-            w[4 * k + 2] = cur[k].z;
-            w[4 * k + 3] = cur[k].w;
-        }
-        P = ge_madd(P, ge_precomp_cneg(ge_precomp_from_words(w), neg_pos ? d > 0 : d < 0));
-#ifndef NW_NO_PREFETCH
-#pragma unroll
-        for (int k = 0; k < 8; ++k) cur[k] = nxt[k];
+        P = ge_madd(P, ge_precomp_cneg(ent30_precomp(cur), neg_pos ? d > 0 : d < 0));
+        cur = nxt;
 #endif
         d = dn;
     }

@@ -153,12 +153,17 @@ NW_HD uint32_t dbl32(uint32_t x) {
 #endif
 }
 
-// Product scanning with the carry fused into the next column (NW_FUSED_CARRY, experimental):
-// column k's multiply-accumulate chain starts from the carry out of column k-1, so the carry
-// needs no separate 64-bit add; the wrap carry (x19) and one 0 -> 1 carry tighten the result.
-// Same bounds as fe_reduce_wide (limb 1 <= 2^25 + 2^18).
-#ifndef NW_FUSED_CARRY
-#define NW_FUSED_CARRY 0
+// Fused-carry product scanning (the mixed addition's products, ge_madd).  Column k of h = f g is
+// ONE v_mad_u64_u32 chain that starts from column k-1's carry (acc = c_{k-1} + sum_i f_i g_{k-i}),
+// so the carry enters as the first MAD's addend instead of a separate 64-bit add; the wrap carry
+// (x19) and one 0 -> 1 carry tighten the result (limb 1 <= 2^25 + 2^18, as fe_reduce_wide).  A lone
+// chain would issue one MAD per dependency latency (and gfx950 needs wait states between dependent
+// 64-bit MADs), so products are only computed this way in groups whose chains interleave MAD by
+// MAD: an empty asm over all accumulators after each step keeps the group in lockstep (without it
+// the scheduler re-serializes the chains).  Measured on MI355X at C2 (profiles/r02/ab_r02k.txt):
+// k_verify 1.176 -> 1.132 ms against operand scanning with a separate carry chain.
+#ifndef NW_MADD_FUSED
+#define NW_MADD_FUSED 1
 #endif
 NW_HD fe fe_fused_wrap(uint32_t r[10], uint64_t c) {
     const uint64_t t = (uint64_t)r[0] + c * 19u;
@@ -170,30 +175,9 @@ NW_HD fe fe_fused_wrap(uint32_t r[10], uint64_t c) {
     return o;
 }
 
-// h = f * g mod p.  Coefficient of f_i g_j: 2 if i, j both odd; x19 if i + j >= 10.
+// h = f * g mod p, operand scanning: ten independent column accumulators (ILP for a lone product),
+// then one carry chain.  Coefficient of f_i g_j: 2 if i, j both odd; x19 if i + j >= 10.
 NW_HD fe fe_mul(const fe& f, const fe& g) {
-#if NW_FUSED_CARRY
-    uint32_t g19[10], f2[10], r[10];
-#pragma unroll
-    for (int j = 0; j < 10; ++j) g19[j] = 19u * g.v[j];
-#pragma unroll
-    for (int i = 0; i < 10; ++i) f2[i] = (i & 1) ? dbl32(f.v[i]) : f.v[i];
-    uint64_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        uint64_t acc = c;
-#pragma unroll
-        for (int i = 0; i < 10; ++i) {
-            const int j = (k - i + 10) % 10;
-            const uint32_t a = ((i & 1) && (j & 1)) ? f2[i] : f.v[i];
-            const uint32_t b = (i + j >= 10) ? g19[j] : g.v[j];
-            acc += (uint64_t)a * b;
-        }
-        r[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
-        c = acc >> ((k & 1) ? 25 : 26);
-    }
-    return fe_fused_wrap(r, c);
-#else
     uint32_t g19[10];
 #pragma unroll
     for (int j = 0; j < 10; ++j) g19[j] = 19u * g.v[j];
@@ -213,32 +197,129 @@ NW_HD fe fe_mul(const fe& f, const fe& g) {
         }
     }
     return fe_reduce_wide(acc);
+}
+
+// Two independent products h1 = f1 g1, h2 = f2 g2 as two interleaved fused-carry chains.
+NW_HD void fe_mul2(fe& h1, const fe& f1, const fe& g1, fe& h2, const fe& f2, const fe& g2) {
+    uint32_t g19a[10], f2a[10], g19b[10], f2b[10], ra[10], rb[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        g19a[j] = 19u * g1.v[j];
+        g19b[j] = 19u * g2.v[j];
+        f2a[j] = (j & 1) ? dbl32(f1.v[j]) : f1.v[j];
+        f2b[j] = (j & 1) ? dbl32(f2.v[j]) : f2.v[j];
+    }
+    uint64_t ca = 0, cb = 0;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        uint64_t acca = ca, accb = cb;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            const int j = (k - i + 10) % 10;
+            const bool dbl = (i & 1) && (j & 1), wrap = i + j >= 10;
+            acca += (uint64_t)(dbl ? f2a[i] : f1.v[i]) * (wrap ? g19a[j] : g1.v[j]);
+            accb += (uint64_t)(dbl ? f2b[i] : f2.v[i]) * (wrap ? g19b[j] : g2.v[j]);
+#if defined(__HIP_DEVICE_COMPILE__)
+            asm volatile("" : "+v"(acca), "+v"(accb));
 #endif
+        }
+        const uint32_t m = (k & 1) ? M25 : M26;
+        const int sh = (k & 1) ? 25 : 26;
+        ra[k] = (uint32_t)acca & m;
+        rb[k] = (uint32_t)accb & m;
+        ca = acca >> sh;
+        cb = accb >> sh;
+    }
+    h1 = fe_fused_wrap(ra, ca);
+    h2 = fe_fused_wrap(rb, cb);
+}
+
+// Three independent products as three interleaved fused-carry chains (NW_MADD3: the mixed
+// addition's first half a, b, c in one group).
+NW_HD void fe_mul3(fe& h1, const fe& f1, const fe& g1, fe& h2, const fe& f2, const fe& g2, fe& h3, const fe& f3,
+                   const fe& g3) {
+    uint32_t a19[10], b19[10], c19[10], fa[10], fb[10], fc[10], r1[10], r2[10], r3[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        a19[j] = 19u * g1.v[j];
+        b19[j] = 19u * g2.v[j];
+        c19[j] = 19u * g3.v[j];
+        fa[j] = (j & 1) ? dbl32(f1.v[j]) : f1.v[j];
+        fb[j] = (j & 1) ? dbl32(f2.v[j]) : f2.v[j];
+        fc[j] = (j & 1) ? dbl32(f3.v[j]) : f3.v[j];
+    }
+    uint64_t c1 = 0, c2 = 0, c3 = 0;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        uint64_t x1 = c1, x2 = c2, x3 = c3;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            const int j = (k - i + 10) % 10;
+            const bool dbl = (i & 1) && (j & 1), wrap = i + j >= 10;
+            x1 += (uint64_t)(dbl ? fa[i] : f1.v[i]) * (wrap ? a19[j] : g1.v[j]);
+            x2 += (uint64_t)(dbl ? fb[i] : f2.v[i]) * (wrap ? b19[j] : g2.v[j]);
+            x3 += (uint64_t)(dbl ? fc[i] : f3.v[i]) * (wrap ? c19[j] : g3.v[j]);
+#if defined(__HIP_DEVICE_COMPILE__)
+            asm volatile("" : "+v"(x1), "+v"(x2), "+v"(x3));
+#endif
+        }
+        const uint32_t m = (k & 1) ? M25 : M26;
+        const int sh = (k & 1) ? 25 : 26;
+        r1[k] = (uint32_t)x1 & m;
+        r2[k] = (uint32_t)x2 & m;
+        r3[k] = (uint32_t)x3 & m;
+        c1 = x1 >> sh;
+        c2 = x2 >> sh;
+        c3 = x3 >> sh;
+    }
+    h1 = fe_fused_wrap(r1, c1);
+    h2 = fe_fused_wrap(r2, c2);
+    h3 = fe_fused_wrap(r3, c3);
+}
+
+// The four products of the mixed addition's second half, X = e f, Y = g h, Z = g f, T = e h, as
+// four interleaved fused-carry chains (dependent MADs 4 apart: no wait states; 19 f, 19 h and the
+// doubled odd limbs of e and g are each computed once).
+NW_HD void fe_mul4_efgh(fe& X, fe& Y, fe& Z, fe& T, const fe& e, const fe& f, const fe& g, const fe& h) {
+    uint32_t f19[10], h19[10], e2[10], g2[10], rx[10], ry[10], rz[10], rt[10];
+#pragma unroll
+    for (int j = 0; j < 10; ++j) {
+        f19[j] = 19u * f.v[j];
+        h19[j] = 19u * h.v[j];
+        e2[j] = (j & 1) ? dbl32(e.v[j]) : e.v[j];
+        g2[j] = (j & 1) ? dbl32(g.v[j]) : g.v[j];
+    }
+    uint64_t cx = 0, cy = 0, cz = 0, ct = 0;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        uint64_t ax = cx, ay = cy, az = cz, at = ct;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            const int j = (k - i + 10) % 10;
+            const bool dbl = (i & 1) && (j & 1), wrap = i + j >= 10;
+            const uint32_t ei = dbl ? e2[i] : e.v[i], gi = dbl ? g2[i] : g.v[i];
+            const uint32_t fj = wrap ? f19[j] : f.v[j], hj = wrap ? h19[j] : h.v[j];
+            ax += (uint64_t)ei * fj;
+            ay += (uint64_t)gi * hj;
+            az += (uint64_t)gi * fj;
+            at += (uint64_t)ei * hj;
+#if defined(__HIP_DEVICE_COMPILE__)
+            asm volatile("" : "+v"(ax), "+v"(ay), "+v"(az), "+v"(at));
+#endif
+        }
+        const uint32_t m = (k & 1) ? M25 : M26;
+        const int sh = (k & 1) ? 25 : 26;
+        rx[k] = (uint32_t)ax & m; ry[k] = (uint32_t)ay & m; rz[k] = (uint32_t)az & m; rt[k] = (uint32_t)at & m;
+        cx = ax >> sh; cy = ay >> sh; cz = az >> sh; ct = at >> sh;
+    }
+    X = fe_fused_wrap(rx, cx);
+    Y = fe_fused_wrap(ry, cy);
+    Z = fe_fused_wrap(rz, cz);
+    T = fe_fused_wrap(rt, ct);
 }
 
 // h = f^2 mod p (55 products).
 NW_HD fe fe_sq(const fe& f) {
-#if NW_FUSED_CARRY
-    uint32_t r[10];
-    uint64_t c = 0;
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        uint64_t acc = c;
-#pragma unroll
-        for (int i = 0; i < 10; ++i) {
-            const int j = (k - i + 10) % 10;
-            if (j < i) continue;   // each unordered pair once
-            uint32_t m1 = (i == j) ? 1u : 2u;
-            if ((i & 1) && (j & 1)) m1 *= 2u;
-            const uint32_t a = f.v[i] * m1;
-            const uint32_t b = (i + j >= 10) ? 19u * f.v[j] : f.v[j];
-            acc += (uint64_t)a * b;
-        }
-        r[k] = (uint32_t)acc & ((k & 1) ? M25 : M26);
-        c = acc >> ((k & 1) ? 25 : 26);
-    }
-    return fe_fused_wrap(r, c);
-#else
     uint64_t acc[10];
 #pragma unroll
     for (int k = 0; k < 10; ++k) acc[k] = 0;
@@ -254,7 +335,6 @@ NW_HD fe fe_sq(const fe& f) {
         }
     }
     return fe_reduce_wide(acc);
-#endif
 }
 
 NW_HD fe fe_sqn(fe f, int n) {

@@ -65,6 +65,9 @@ NW_HD ge_precomp ge_precomp_identity() {
     return r;
 }
 
+#ifndef NW_MADD3
+#define NW_MADD3 0
+#endif
 #if NW_HALF_NIELS
 // p + q (mixed, halved entry).  The HWCD formulas with every quantity halved: A/2 = (Y1-X1)(y-x)/2,
 // B/2, C/2 = T1 d x y, D/2 = Z1 (no doubling), E/2, F/2 = Z1 - C/2, G/2, H/2; the products
@@ -75,18 +78,33 @@ NW_HD ge_precomp ge_precomp_identity() {
 // e = b - a loose (k = 5, first operands only), f k=3, g = Z1 + C/2 k=2, h = b + a k=2; products
 // e f 15, g h 4, g f 6, e h 10 <= 32.  xy2d (d x y) may be k=2 (negated entry).
 NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) {
+#if NW_MADD_FUSED && NW_MADD3
+    fe a, b, c;
+    fe_mul3(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx, c, p.T, q.xy2d);
+#elif NW_MADD_FUSED
+    // a and b as one interleaved pair; c alone by operand scanning (a lone fused chain would stall;
+    // a three-way group spills at the 168-VGPR bound)
+    fe a, b;
+    fe_mul2(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx);
+    const fe c = fe_mul(p.T, q.xy2d);
+#else
     const fe a = fe_mul(fe_sub_loose(p.Y, p.X), q.ymx);
     const fe b = fe_mul(fe_add(p.Y, p.X), q.ypx);
     const fe c = fe_mul(p.T, q.xy2d);
+#endif
     const fe e = fe_sub_loose(b, a);
     const fe h = fe_add(b, a);
     const fe f = fe_sub2p_loose(p.Z, c);
     const fe g = fe_add(p.Z, c);
     ge_p3 r;
+#if NW_MADD_FUSED
+    fe_mul4_efgh(r.X, r.Y, r.Z, r.T, e, f, g, h);
+#else
     r.X = fe_mul(e, f);
     r.Y = fe_mul(g, h);
     r.Z = fe_mul(g, f);
     r.T = fe_mul(e, h);
+#endif
     return r;
 }
 

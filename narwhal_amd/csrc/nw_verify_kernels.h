@@ -46,6 +46,9 @@ __device__ __forceinline__ void coeff_z(const VerifyParams& a, uint32_t i, uint3
 // Occupancy: the 32-byte-digest kernel (certificates, votes, headers: the hot path) is held to
 // 168 VGPRs = 3 waves per SIMD (a few spills, measured faster than 2 waves at 169-175 VGPRs).
 // The generic-message kernel (worker chunks) is left unbounded: bounding it spills heavily.
+#ifndef NW_H_LDS
+#define NW_H_LDS 0
+#endif
 #ifndef NW_VERIFY_WAVES
 #define NW_VERIFY_WAVES 3
 #endif
@@ -68,7 +71,28 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     }
     uint32_t* frow = a.pbuf + (size_t)PREC_FLAGS_ROW * a.n;
     frow[gid] = flags;   // parked (coalesced) so neither flags nor i stays live through the combs
+#if NW_H_LDS
+    // h parked in LDS through the basepoint pass (8 VGPRs fewer at the loop's peak)
+    __shared__ uint32_t h_park[8][256];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h_park[k][threadIdx.x] = h[k];
+    ge_p3 P;
+    {
+        uint32_t s_use[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s_use[k] = sok ? S[k] : 0u;
+        comb_pass<B_WINDOW, true>(P, s_use, a.btab, false);
+    }
+    asm volatile("" ::: "memory");
+    {
+        uint32_t h2[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h2[k] = h_park[k][threadIdx.x];
+        comb_pass<WA, false>(P, h2, a.key_tab + (size_t)slot * comb_words(WA), true);
+    }
+#else
     const ge_p3 P = compute_P<WA>(S, h, sok, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
+#endif
     // X, Z and the partial flags (y match, R sign, R small) in processing order, struct-of-arrays
     // (column gid): coalesced for k_finish, which completes the flags and writes flags[i].  R, i
     // and flags are re-read here rather than kept live through the combs (10 VGPRs): that keeps
