@@ -440,7 +440,8 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
                   size_t nsigs, const uint8_t* d_sig, const uint32_t* d_signer, int msgmode, const uint8_t* d_msg32,
                   const uint8_t* d_msg_base, const uint64_t* d_msg_off, const uint64_t* d_msg_len,
                   const uint8_t* zseed, uint64_t cert_base, uint32_t batch_mode, uint8_t* d_cert_ok,
-                  uint32_t* d_flags_user, uint64_t* d_stake_out, hipStream_t st, uint8_t* d_sig_ok = nullptr) {
+                  uint32_t* d_flags_user, uint64_t* d_stake_out, hipStream_t st, uint8_t* d_sig_ok = nullptr,
+                  uint32_t* d_status = nullptr) {
     uint32_t* d_flags = d_flags_user;
     if (!d_flags) {
         NW_TRY(ws->ensure(ws->w_flags, nsigs * 4 + 4), "ws flags");
@@ -453,11 +454,21 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     if (batch_mode) NW_TRY(ws->ensure(ws->w_slow_buf, nsigs * (size_t)SLOW_WORDS * 4 + 4), "ws slow_buf");
     NW_TRY(ws->ensure(ws->w_pbuf, nsigs * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
     NW_TRY(ws->ensure(ws->w_pre, nsigs * 40 + 16), "ws pre");
-    // votes not covered by any certificate map to certificate 0 (never out of range)
-    NW_TRY(hipMemsetAsync(ws->w_sig_cert.p, 0, nsigs * 4 + 4, st), "memset sig_cert");
-    NW_TRY(launch_expand_certs((uint32_t)ncerts, (uint32_t)nsigs, d_first, d_nv, ws->w_sig_cert.as<uint32_t>(),
-                               ws->w_slow_count.as<uint32_t>(), st),
-           "k_expand_certs");   // also zeroes the slow-path counter
+    // signer grouping (device counting sort) when keys repeat
+    const bool group = !ctx->group_off && nsigs >= kGroupMinSigs && ctx->nkeys > 1 &&
+                       nsigs >= kGroupMinSigsPerKey * ctx->nkeys;
+    if (group) {
+        NW_TRY(ws->ensure(ws->w_counts, ctx->nkeys * 4 + 16), "ws counts");
+        NW_TRY(ws->ensure(ws->w_cursor, ctx->nkeys * 4 + 16), "ws cursor");
+        NW_TRY(ws->ensure(ws->w_perm, nsigs * 4 + 16), "ws perm");
+    }
+    // Preamble in two launches: zero sig_cert (votes outside every certificate map to certificate
+    // 0), the slot counts, the slow-path counter and d_status; expand certificates; histogram
+    // signer slots; check the device inputs into d_status (when given).
+    NW_TRY(launch_prep_expand((uint32_t)ncerts, (uint32_t)nsigs, (uint32_t)ctx->nkeys, d_first, d_nv, d_signer,
+                              ws->w_sig_cert.as<uint32_t>(), ws->w_slow_count.as<uint32_t>(),
+                              group ? ws->w_counts.as<uint32_t>() : nullptr, d_status, st),
+           "k_prep_certs / k_expand_count");
 
     VerifyParams vp{};
     vp.n = (uint32_t)nsigs;
@@ -486,12 +497,9 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     vp.pbuf = ws->w_pbuf.as<uint32_t>();
     vp.pre = ws->w_pre.as<uint32_t>();
     vp.perm = nullptr;
-    if (!ctx->group_off && nsigs >= kGroupMinSigs && ctx->nkeys > 1 && nsigs >= kGroupMinSigsPerKey * ctx->nkeys) {
-        NW_TRY(ws->ensure(ws->w_counts, ctx->nkeys * 4 + 16), "ws counts");
-        NW_TRY(ws->ensure(ws->w_cursor, ctx->nkeys * 4 + 16), "ws cursor");
-        NW_TRY(ws->ensure(ws->w_perm, nsigs * 4 + 16), "ws perm");
-        NW_TRY(launch_group_by_signer((uint32_t)nsigs, (uint32_t)ctx->nkeys, d_signer, ws->w_counts.as<uint32_t>(),
-                                      ws->w_cursor.as<uint32_t>(), ws->w_perm.as<uint32_t>(), st),
+    if (group) {
+        NW_TRY(launch_group_scatter((uint32_t)nsigs, (uint32_t)ctx->nkeys, d_signer, ws->w_counts.as<uint32_t>(),
+                                    ws->w_cursor.as<uint32_t>(), ws->w_perm.as<uint32_t>(), st),
                "signer grouping");
         vp.perm = ws->w_perm.as<uint32_t>();
     }
@@ -1221,16 +1229,15 @@ int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first
     NW_TRY(lease.bind(st, false), "hipStreamWaitEvent");
     // input validation on the device (the inputs are device-resident); every kernel below also
     // clamps them, so invalid inputs never fault
-    uint32_t* status = d_status;
-    if (!status) {
-        NW_TRY(ws->ensure(ws->w_status, 16), "ws status");
-        status = ws->w_status.as<uint32_t>();
-    }
-    NW_TRY(hipMemsetAsync(status, 0, 4, st), "memset status");
-    NW_TRY(launch_validate_certs((uint32_t)ncerts, (uint32_t)nsigs, (uint32_t)ctx->nkeys, d_cert_first,
-                                 d_cert_nvotes, d_signer_slot, status, st),
-           "k_validate_certs");
+    // With d_status the check runs inside the batch preamble (k_expand_count) in stream order;
+    // without it the call validates first and waits for the verdict.
     if (!d_status) {   // synchronous validation: NW_ERR_ARG before any verification is enqueued
+        NW_TRY(ws->ensure(ws->w_status, 16), "ws status");
+        uint32_t* status = ws->w_status.as<uint32_t>();
+        NW_TRY(hipMemsetAsync(status, 0, 4, st), "memset status");
+        NW_TRY(launch_validate_certs((uint32_t)ncerts, (uint32_t)nsigs, (uint32_t)ctx->nkeys, d_cert_first,
+                                     d_cert_nvotes, d_signer_slot, status, st),
+               "k_validate_certs");
         NW_TRY(ws->h_io.ensure(16), "pinned status");
         NW_TRY(hipMemcpyAsync(ws->h_io.p, status, 4, hipMemcpyDeviceToHost, st), "D2H status");
         NW_TRY(hipStreamSynchronize(st), "sync(status)");
@@ -1244,7 +1251,7 @@ int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first
     }
     int rc = enqueue_certs(ctx, ws, ncerts, d_cert_first, d_cert_nvotes, nsigs, d_sig64, d_signer_slot, 0, d_msg32,
                            nullptr, nullptr, nullptr, zseed, cert_base, 1, d_cert_ok, d_sig_flags, d_accepted_stake,
-                           st);
+                           st, nullptr, d_status);
     NW_TRY(lease.finish(), "hipEventRecord");
     return rc;
 }

@@ -68,13 +68,16 @@ struct FinalizeParams {
 
 hipError_t launch_verify(const VerifyParams& p, int msgmode, int key_window, hipStream_t st);
 hipError_t launch_finish(const VerifyParams& p, hipStream_t st);
-hipError_t launch_group_by_signer(uint32_t n, uint32_t nkeys, const uint32_t* signer, uint32_t* counts,
-                                  uint32_t* cursor, uint32_t* perm, hipStream_t st);
 hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st);
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st);
-// Also zeroes zero4[0..3] (the slow-path counter) when ncerts > 0, saving a memset launch.
-hipError_t launch_expand_certs(uint32_t ncerts, uint32_t nsigs, const uint32_t* first, const uint32_t* nv,
-                               uint32_t* sig_cert, uint32_t* zero4, hipStream_t st);
+// Batch preamble: zero sig_cert / counts (may be null: no histogram) / the slow counter / status (may
+// be null: no input check), expand certificates, histogram + check signer slots (k_prep_certs,
+// k_expand_count); then launch_group_scatter (scan + scatter) when counts were built.
+hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
+                              const uint32_t* nv, const uint32_t* signer, uint32_t* sig_cert, uint32_t* zero4,
+                              uint32_t* counts, uint32_t* status, hipStream_t st);
+hipError_t launch_group_scatter(uint32_t n, uint32_t nkeys, const uint32_t* signer, const uint32_t* counts,
+                                uint32_t* cursor, uint32_t* perm, hipStream_t st);
 hipError_t launch_validate_certs(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
                                  const uint32_t* nv, const uint32_t* signer, uint32_t* status, hipStream_t st);
 hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hipStream_t st);

@@ -13,10 +13,11 @@
 // evaluates the remaining terms literally.  Verdicts are therefore identical to dalek's for every
 // input (not just honest ones) given the same z_i.
 //
-// Pipeline per batch: k_expand_certs -> [signer grouping] -> k_verify (P_i, one lane per signature)
+// Pipeline per batch: k_prep_certs + k_expand_count -> [signer grouping] -> k_verify (P_i, one lane per signature)
 // -> k_finish (Montgomery batch inversion of Z over FINISH_K signatures per lane, encoding match,
 // strict verdict) -> k_slow_sig (compacted list of mismatches only) -> k_cert_finalize.
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include "nw_point.h"
 #include "nw_sha512.h"
 #include "nw_kernels.h"
@@ -43,25 +44,6 @@ static constexpr uint32_t GROUP_LDS_KEYS = 8192;
 
 // Out-of-range slots (rejected by k_verify) are grouped with slot 0 so no access leaves the arrays.
 __device__ __forceinline__ uint32_t clamp_slot(uint32_t s, uint32_t nkeys) { return s < nkeys ? s : 0u; }
-
-__global__ void __launch_bounds__(256) k_count_slots(uint32_t n, uint32_t nkeys, const uint32_t* signer,
-                                                     uint32_t* counts) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) atomicAdd(&counts[clamp_slot(signer[i], nkeys)], 1u);
-}
-
-__global__ void __launch_bounds__(256) k_count_slots_lds(uint32_t n, uint32_t nkeys, const uint32_t* signer,
-                                                         uint32_t* counts) {
-    extern __shared__ uint32_t hist[];
-    for (uint32_t k = threadIdx.x; k < nkeys; k += blockDim.x) hist[k] = 0;
-    __syncthreads();
-    const uint32_t t0 = blockIdx.x * GROUP_TILE;
-    const uint32_t t1 = min(n, t0 + GROUP_TILE);
-    for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) atomicAdd(&hist[clamp_slot(signer[i], nkeys)], 1u);
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nkeys; k += blockDim.x)
-        if (hist[k]) atomicAdd(&counts[k], hist[k]);
-}
 
 // Single-block exclusive scan of counts[0..k) into cursor[0..k).
 __global__ void __launch_bounds__(1024) k_scan_slots(uint32_t k, const uint32_t* counts, uint32_t* cursor) {
@@ -236,16 +218,6 @@ __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
     if (a.accepted_stake) a.accepted_stake[c] = stake;
 }
 
-__global__ void __launch_bounds__(256) k_expand_certs(uint32_t ncerts, uint32_t nsigs, const uint32_t* cert_first,
-                                                      const uint32_t* cert_n, uint32_t* sig_cert, uint32_t* zero4) {
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c < 4) zero4[c] = 0u;   // ncerts >= 1: the launch has at least 256 threads
-    if (c >= ncerts) return;
-    const uint32_t f = cert_first[c], n = cert_n[c];
-    const uint32_t end = (uint64_t)f + n > nsigs ? nsigs : f + n;   // clamped: k_cert_finalize rejects
-    for (uint32_t v = f; v < end; ++v) sig_cert[v] = c;
-}
-
 // Device-side input check of nw_verify_certs_dev: every vote range inside [0, nsigs) and every
 // signer slot inside the key cache; *status |= NW_ERR_ARG otherwise (the verify kernels clamp the
 // same inputs, so a bad call never reads outside its arrays).
@@ -257,6 +229,64 @@ __global__ void __launch_bounds__(256) k_validate_certs(uint32_t ncerts, uint32_
     if (t < ncerts) bad = (uint64_t)cert_first[t] + cert_n[t] > nsigs;
     if (t < nsigs) bad = bad || signer[t] >= nkeys;
     if (bad) atomicOr(status, (uint32_t)NW_ERR_ARG);
+}
+
+// ------------------------------------------------------------------------------------ batch preamble
+// Two launches replace the five small ones a certificate batch used to start with (status /
+// sig_cert / slot-count fills, input check, certificate expansion, slot histogram): ~5 us each on
+// MI355X, dominated by dispatch, not work.
+//   k_prep_certs:   sig_cert = 0 (votes outside every certificate map to certificate 0), the slot
+//                   counts, the slow-path counter and the status word = 0.
+//   k_expand_count: block b expands certificates [256 b, 256 b + 256) into sig_cert and, for
+//                   signature tile b (GROUP_TILE signatures), histograms the signer slots (LDS, one
+//                   global add per slot) and/or checks them; every check ORs NW_ERR_ARG into status.
+__global__ void __launch_bounds__(256) k_prep_certs(uint32_t nsigs, uint32_t nkeys, uint32_t* sig_cert, uint32_t* counts,
+                                                    uint32_t* zero4, uint32_t* status) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = t; i <= nsigs; i += stride) sig_cert[i] = 0u;
+    if (counts)
+        for (uint32_t k = t; k < nkeys; k += stride) counts[k] = 0u;
+    if (t < 4) zero4[t] = 0u;
+    if (status && t == 0) *status = 0u;
+}
+
+__global__ void __launch_bounds__(256) k_expand_count(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys,
+                                                      const uint32_t* cert_first, const uint32_t* cert_n,
+                                                      const uint32_t* signer, uint32_t* sig_cert, uint32_t* counts,
+                                                      uint32_t* status) {
+    extern __shared__ uint32_t hist[];
+    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    bool bad = false;
+    if (c < ncerts) {
+        const uint32_t f = cert_first[c], n = cert_n[c];
+        bad = (uint64_t)f + n > nsigs;
+        const uint32_t end = bad ? nsigs : f + n;   // clamped: k_cert_finalize rejects it anyway
+        for (uint32_t v = f; v < end; ++v) sig_cert[v] = c;
+    }
+    const uint32_t t0 = blockIdx.x * GROUP_TILE;
+    if ((counts || status) && t0 < nsigs) {
+        const uint32_t t1 = min(nsigs, t0 + GROUP_TILE);
+        const bool lds = counts && nkeys <= GROUP_LDS_KEYS;
+        if (lds) {
+            for (uint32_t k = threadIdx.x; k < nkeys; k += blockDim.x) hist[k] = 0;
+            __syncthreads();
+        }
+        for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
+            const uint32_t sl = signer[i];
+            bad = bad || sl >= nkeys;
+            if (lds)
+                atomicAdd(&hist[clamp_slot(sl, nkeys)], 1u);
+            else if (counts)
+                atomicAdd(&counts[clamp_slot(sl, nkeys)], 1u);
+        }
+        if (lds) {
+            __syncthreads();
+            for (uint32_t k = threadIdx.x; k < nkeys; k += blockDim.x)
+                if (hist[k]) atomicAdd(&counts[k], hist[k]);
+        }
+    }
+    if (bad && status) atomicOr(status, (uint32_t)NW_ERR_ARG);
 }
 
 __global__ void __launch_bounds__(256) k_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok) {
@@ -359,27 +389,6 @@ hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint3
     return launch_vs(p, msgmode, key_window, true, n_upper, st);
 }
 
-hipError_t launch_group_by_signer(uint32_t n, uint32_t nkeys, const uint32_t* signer, uint32_t* counts,
-                                  uint32_t* cursor, uint32_t* perm, hipStream_t st) {
-    if (n == 0 || nkeys == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(counts, 0, (size_t)nkeys * 4, st);
-    if (e != hipSuccess) return e;
-    const bool lds = nkeys <= GROUP_LDS_KEYS;
-    if (lds)
-        hipLaunchKernelGGL(k_count_slots_lds, dim3(blocks_for(n, GROUP_TILE)), dim3(256), nkeys * 4, st, n, nkeys,
-                           signer, counts);
-    else
-        hipLaunchKernelGGL(k_count_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, nkeys, signer, counts);
-    hipLaunchKernelGGL(k_scan_slots, dim3(1), dim3(1024), 0, st, nkeys, counts, cursor);
-    if (lds)
-        hipLaunchKernelGGL(k_scatter_slots_lds, dim3(blocks_for(n, GROUP_TILE)), dim3(256), nkeys * 8, st, n, nkeys,
-                           signer, cursor, perm);
-    else
-        hipLaunchKernelGGL(k_scatter_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, nkeys, signer, cursor,
-                           perm);
-    return hipGetLastError();
-}
-
 hipError_t launch_finish(const VerifyParams& p, hipStream_t st) {
     if (p.gn == 0) return hipSuccess;
     if (p.fk < 1 || p.fk > (uint32_t)FINISH_K || (uint64_t)p.g0 + p.gn > p.n) return hipErrorInvalidValue;
@@ -394,11 +403,31 @@ hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_expand_certs(uint32_t ncerts, uint32_t nsigs, const uint32_t* first, const uint32_t* nv,
-                               uint32_t* sig_cert, uint32_t* zero4, hipStream_t st) {
-    if (ncerts == 0) return hipMemsetAsync(zero4, 0, 16, st);
-    hipLaunchKernelGGL(k_expand_certs, dim3(blocks_for(ncerts, 256)), dim3(256), 0, st, ncerts, nsigs, first, nv,
-                       sig_cert, zero4);
+hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
+                              const uint32_t* nv, const uint32_t* signer, uint32_t* sig_cert, uint32_t* zero4,
+                              uint32_t* counts, uint32_t* status, hipStream_t st) {
+    const uint32_t prep_blocks = std::min<uint32_t>(blocks_for(nsigs + 1, 256), 1024u);
+    hipLaunchKernelGGL(k_prep_certs, dim3(prep_blocks), dim3(256), 0, st, nsigs, nkeys, sig_cert, counts, zero4, status);
+    const bool tiles = (counts || status) && nsigs > 0;
+    const uint32_t nb = std::max<uint32_t>(blocks_for(ncerts, 256), tiles ? blocks_for(nsigs, GROUP_TILE) : 0u);
+    if (nb == 0) return hipGetLastError();
+    const size_t lds = counts && nkeys <= GROUP_LDS_KEYS ? (size_t)nkeys * 4 : 0;
+    hipLaunchKernelGGL(k_expand_count, dim3(nb), dim3(256), lds, st, ncerts, nsigs, nkeys, first, nv, signer, sig_cert,
+                       counts, status);
+    return hipGetLastError();
+}
+
+// Scan + scatter of the signer grouping whose counts k_expand_count produced.
+hipError_t launch_group_scatter(uint32_t n, uint32_t nkeys, const uint32_t* signer, const uint32_t* counts,
+                                uint32_t* cursor, uint32_t* perm, hipStream_t st) {
+    if (n == 0 || nkeys == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scan_slots, dim3(1), dim3(1024), 0, st, nkeys, counts, cursor);
+    if (nkeys <= GROUP_LDS_KEYS)
+        hipLaunchKernelGGL(k_scatter_slots_lds, dim3(blocks_for(n, GROUP_TILE)), dim3(256), nkeys * 8, st, n, nkeys,
+                           signer, cursor, perm);
+    else
+        hipLaunchKernelGGL(k_scatter_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, nkeys, signer, cursor,
+                           perm);
     return hipGetLastError();
 }
 
