@@ -160,7 +160,9 @@ NW_HD ge_precomp ent30_precomp(const ent30& e) {
 // field arithmetic.  neg_pos: negate entries for positive digits (-h A).  FIRST: P is the identity
 // on entry, so position 0's entry becomes P directly (ge_from_precomp: 1 multiplication, not 7).
 // (Measured and rejected: two positions per iteration with two alternating buffers, to drop the
-// buffer copy: it spills at the 168-VGPR bound.)
+// buffer copy: it spills at the 168-VGPR bound; issuing the gather between the two halves of the
+// addition (ge_madd_s1 / ge_madd_s2) to free the buffer's registers for a three-product first half:
+// that still spills.)
 template <int W, bool FIRST>
 NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab, bool neg_pos) {
     int carry = 0;

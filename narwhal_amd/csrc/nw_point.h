@@ -77,13 +77,17 @@ NW_HD ge_precomp ge_precomp_identity() {
 // fe_mul operand (19 F/2 < 2^32) without carrying.  Limb budget: (Y1+X1) k=2, (Y1-X1) and
 // e = b - a loose (k = 5, first operands only), f k=3, g = Z1 + C/2 k=2, h = b + a k=2; products
 // e f 15, g h 4, g f 6, e h 10 <= 32.  xy2d (d x y) may be k=2 (negated entry).
-NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) {
+// The two halves of the mixed addition: a, b, c and the sums e, f, g, h; then the four products.
+struct madd_mid {
+    fe e, f, g, h;
+};
+
+NW_HD madd_mid ge_madd_s1(const ge_p3& p, const ge_precomp& q) {
 #if NW_MADD_FUSED && NW_MADD3
     fe a, b, c;
     fe_mul3(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx, c, p.T, q.xy2d);
 #elif NW_MADD_FUSED
-    // a and b as one interleaved pair; c alone by operand scanning (a lone fused chain would stall;
-    // a three-way group spills at the 168-VGPR bound)
+    // a and b as one interleaved pair; c alone by operand scanning (a lone fused chain would stall)
     fe a, b;
     fe_mul2(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx);
     const fe c = fe_mul(p.T, q.xy2d);
@@ -92,21 +96,28 @@ NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) {
     const fe b = fe_mul(fe_add(p.Y, p.X), q.ypx);
     const fe c = fe_mul(p.T, q.xy2d);
 #endif
-    const fe e = fe_sub_loose(b, a);
-    const fe h = fe_add(b, a);
-    const fe f = fe_sub2p_loose(p.Z, c);
-    const fe g = fe_add(p.Z, c);
+    madd_mid m;
+    m.e = fe_sub_loose(b, a);
+    m.h = fe_add(b, a);
+    m.f = fe_sub2p_loose(p.Z, c);
+    m.g = fe_add(p.Z, c);
+    return m;
+}
+
+NW_HD ge_p3 ge_madd_s2(const madd_mid& m) {
     ge_p3 r;
 #if NW_MADD_FUSED
-    fe_mul4_efgh(r.X, r.Y, r.Z, r.T, e, f, g, h);
+    fe_mul4_efgh(r.X, r.Y, r.Z, r.T, m.e, m.f, m.g, m.h);
 #else
-    r.X = fe_mul(e, f);
-    r.Y = fe_mul(g, h);
-    r.Z = fe_mul(g, f);
-    r.T = fe_mul(e, h);
+    r.X = fe_mul(m.e, m.f);
+    r.Y = fe_mul(m.g, m.h);
+    r.Z = fe_mul(m.g, m.f);
+    r.T = fe_mul(m.e, m.h);
 #endif
     return r;
 }
+
+NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) { return ge_madd_s2(ge_madd_s1(p, q)); }
 
 // Extended point of a halved affine Niels entry, with no field multiplication beyond T:
 // X = (y+x)/2 - (y-x)/2 = x, Y = y, Z = 1, T = xy = (d x y) / d.
