@@ -163,7 +163,7 @@ NW_HD ge_precomp ent30_precomp(const ent30& e) {
 // buffer copy: it spills at the 168-VGPR bound; issuing the gather between the two halves of the
 // addition (ge_madd_s1 / ge_madd_s2) to free the buffer's registers for a three-product first half:
 // that still spills.)
-template <int W, bool FIRST>
+template <int W, bool FIRST, bool FUSED = false>
 NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab, bool neg_pos) {
     int carry = 0;
     int d = next_digit<W>(sc, carry);
@@ -184,14 +184,14 @@ NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab,
 #ifdef NW_NO_PREFETCH
         cur = load_ent30(tab + ((size_t)pos * comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
         if (pos + 1 < comb_pos(W)) dn = next_digit<W>(sc, carry);
-        P = ge_madd(P, ge_precomp_cneg(ent30_precomp(cur), neg_pos ? d > 0 : d < 0));
+        P = ge_madd<FUSED>(P, ge_precomp_cneg(ent30_precomp(cur), neg_pos ? d > 0 : d < 0));
 #else
         ent30 nxt;
         if (pos + 1 < comb_pos(W)) {
             dn = next_digit<W>(sc, carry);
             nxt = load_ent30(tab + ((size_t)(pos + 1) * comb_ent(W) + (dn < 0 ? -dn : dn)) * PRECOMP_WORDS);
         }
-        P = ge_madd(P, ge_precomp_cneg(ent30_precomp(cur), neg_pos ? d > 0 : d < 0));
+        P = ge_madd<FUSED>(P, ge_precomp_cneg(ent30_precomp(cur), neg_pos ? d > 0 : d < 0));
         cur = nxt;
 #endif
         d = dn;
@@ -200,7 +200,7 @@ NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab,
 
 // P = s B - h A: radix-2^WB comb over the basepoint table, then radix-2^WA comb over the key
 // table (WA = 0: s B only).  Each step is one gather + one mixed addition, no doublings.
-template <int WB, int WA>
+template <int WB, int WA, bool FUSED = false>
 NW_HD ge_p3 comb_sB_minus_hA(const uint32_t s_in[8], const uint32_t h_in[8], const uint32_t* __restrict__ btab,
                              const uint32_t* __restrict__ atab) {
     uint32_t s[8], h[8];
@@ -210,8 +210,8 @@ NW_HD ge_p3 comb_sB_minus_hA(const uint32_t s_in[8], const uint32_t h_in[8], con
         h[k] = h_in[k];
     }
     ge_p3 P;
-    comb_pass<WB, true>(P, s, btab, false);
-    if constexpr (WA > 0) comb_pass<WA, false>(P, h, atab, true);
+    comb_pass<WB, true, FUSED>(P, s, btab, false);
+    if constexpr (WA > 0) comb_pass<WA, false, FUSED>(P, h, atab, true);
     return P;
 }
 
@@ -230,13 +230,13 @@ NW_HD void hram_msg32(uint32_t h[8], const uint32_t R[8], const uint32_t A[8], c
 }
 
 // P = s B - h A (s forced to 0 when non-canonical so the comb's digit range stays valid).
-template <int WA, int WB = B_WINDOW>
+template <int WA, int WB = B_WINDOW, bool FUSED = false>
 NW_HD ge_p3 compute_P(const uint32_t S[8], const uint32_t h[8], bool sok, const uint32_t* btab,
                       const uint32_t* atab) {
     uint32_t s_use[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) s_use[k] = sok ? S[k] : 0u;
-    return comb_sB_minus_hA<WB, WA>(s_use, h, btab, atab);
+    return comb_sB_minus_hA<WB, WA, FUSED>(s_use, h, btab, atab);
 }
 
 NW_HD fe load_fe(const uint32_t* p) {

@@ -163,7 +163,7 @@ NW_HD uint32_t dbl32(uint32_t x) {
 // the scheduler re-serializes the chains).  Measured on MI355X at C2 (profiles/r02/ab_r02k.txt):
 // k_verify 1.176 -> 1.132 ms against operand scanning with a separate carry chain.
 #ifndef NW_MADD_FUSED
-#define NW_MADD_FUSED 1
+#define NW_MADD_FUSED 1   // 0: k_verify's throughput kernel uses operand-scanned products too (A/B)
 #endif
 NW_HD fe fe_fused_wrap(uint32_t r[10], uint64_t c) {
     const uint64_t t = (uint64_t)r[0] + c * 19u;

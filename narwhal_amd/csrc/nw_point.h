@@ -82,42 +82,57 @@ struct madd_mid {
     fe e, f, g, h;
 };
 
+// FUSED selects the fused-carry product groups (fe_mul2 / fe_mul4_efgh).  They pay off only where
+// several waves share a SIMD (k_verify's throughput kernel, 3 waves): at one wave per SIMD the
+// lockstep chains expose their MAD latency and the operand-scanned products are faster (worker
+// chunks, k_verify<1,W>: 98 vs 62-85 M sigs/s; profiles/r02/ab_r02.txt r02t).
+template <bool FUSED>
 NW_HD madd_mid ge_madd_s1(const ge_p3& p, const ge_precomp& q) {
-#if NW_MADD_FUSED && NW_MADD3
-    fe a, b, c;
-    fe_mul3(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx, c, p.T, q.xy2d);
-#elif NW_MADD_FUSED
-    // a and b as one interleaved pair; c alone by operand scanning (a lone fused chain would stall)
-    fe a, b;
-    fe_mul2(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx);
-    const fe c = fe_mul(p.T, q.xy2d);
-#else
-    const fe a = fe_mul(fe_sub_loose(p.Y, p.X), q.ymx);
-    const fe b = fe_mul(fe_add(p.Y, p.X), q.ypx);
-    const fe c = fe_mul(p.T, q.xy2d);
-#endif
     madd_mid m;
-    m.e = fe_sub_loose(b, a);
-    m.h = fe_add(b, a);
-    m.f = fe_sub2p_loose(p.Z, c);
-    m.g = fe_add(p.Z, c);
+    if constexpr (FUSED && NW_MADD3) {
+        fe a, b, c;
+        fe_mul3(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx, c, p.T, q.xy2d);
+        m.e = fe_sub_loose(b, a);
+        m.h = fe_add(b, a);
+        m.f = fe_sub2p_loose(p.Z, c);
+        m.g = fe_add(p.Z, c);
+    } else if constexpr (FUSED) {
+        // a and b as one interleaved pair; c alone by operand scanning (a lone fused chain stalls)
+        fe a, b;
+        fe_mul2(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx);
+        const fe c = fe_mul(p.T, q.xy2d);
+        m.e = fe_sub_loose(b, a);
+        m.h = fe_add(b, a);
+        m.f = fe_sub2p_loose(p.Z, c);
+        m.g = fe_add(p.Z, c);
+    } else {
+        const fe a = fe_mul(fe_sub_loose(p.Y, p.X), q.ymx);
+        const fe b = fe_mul(fe_add(p.Y, p.X), q.ypx);
+        const fe c = fe_mul(p.T, q.xy2d);
+        m.e = fe_sub_loose(b, a);
+        m.h = fe_add(b, a);
+        m.f = fe_sub2p_loose(p.Z, c);
+        m.g = fe_add(p.Z, c);
+    }
     return m;
 }
 
+template <bool FUSED>
 NW_HD ge_p3 ge_madd_s2(const madd_mid& m) {
     ge_p3 r;
-#if NW_MADD_FUSED
-    fe_mul4_efgh(r.X, r.Y, r.Z, r.T, m.e, m.f, m.g, m.h);
-#else
-    r.X = fe_mul(m.e, m.f);
-    r.Y = fe_mul(m.g, m.h);
-    r.Z = fe_mul(m.g, m.f);
-    r.T = fe_mul(m.e, m.h);
-#endif
+    if constexpr (FUSED) {
+        fe_mul4_efgh(r.X, r.Y, r.Z, r.T, m.e, m.f, m.g, m.h);
+    } else {
+        r.X = fe_mul(m.e, m.f);
+        r.Y = fe_mul(m.g, m.h);
+        r.Z = fe_mul(m.g, m.f);
+        r.T = fe_mul(m.e, m.h);
+    }
     return r;
 }
 
-NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) { return ge_madd_s2(ge_madd_s1(p, q)); }
+template <bool FUSED = false>
+NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) { return ge_madd_s2<FUSED>(ge_madd_s1<FUSED>(p, q)); }
 
 // Extended point of a halved affine Niels entry, with no field multiplication beyond T:
 // X = (y+x)/2 - (y-x)/2 = x, Y = y, Z = 1, T = xy = (d x y) / d.
@@ -134,6 +149,7 @@ NW_HD ge_p3 ge_from_precomp(const ge_precomp& q) {
 // p + q (mixed).  Limb budget: (Y1+X1) k=2, D = 2Z1 k=2, G = D + C k=3, xy2d may be k=2 (negated).
 // (Y1-X1) and e = b - a skip the carry pass (fe_sub_loose, k = 5): each only ever feeds fe_mul as
 // the first operand against a second operand of k <= 2 (ymx tight; f tight; h k=2): 5 x 2 <= 32.
+template <bool FUSED = false>
 NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) {
     const fe a = fe_mul(fe_sub_loose(p.Y, p.X), q.ymx);
     const fe b = fe_mul(fe_add(p.Y, p.X), q.ypx);

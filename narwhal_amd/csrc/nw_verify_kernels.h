@@ -81,17 +81,19 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
         uint32_t s_use[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) s_use[k] = sok ? S[k] : 0u;
-        comb_pass<B_WINDOW, true>(P, s_use, a.btab, false);
+        comb_pass<B_WINDOW, true, MSGMODE == 0 && NW_MADD_FUSED>(P, s_use, a.btab, false);
     }
     asm volatile("" ::: "memory");
     {
         uint32_t h2[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) h2[k] = h_park[k][threadIdx.x];
-        comb_pass<WA, false>(P, h2, a.key_tab + (size_t)slot * comb_words(WA), true);
+        comb_pass<WA, false, MSGMODE == 0 && NW_MADD_FUSED>(P, h2, a.key_tab + (size_t)slot * comb_words(WA), true);
     }
 #else
-    const ge_p3 P = compute_P<WA>(S, h, sok, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
+    // fused-carry products only in the 3-waves-per-SIMD kernel (MSGMODE 0); see ge_madd_s1
+    const ge_p3 P = compute_P<WA, B_WINDOW, MSGMODE == 0 && NW_MADD_FUSED>(S, h, sok, a.btab,
+                                                                           a.key_tab + (size_t)slot * comb_words(WA));
 #endif
     // X, Z and the partial flags (y match, R sign, R small) in processing order, struct-of-arrays
     // (column gid): coalesced for k_finish, which completes the flags and writes flags[i].  R, i
