@@ -198,6 +198,36 @@ NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab,
     }
 }
 
+// comb_pass with the signed digits precomputed (dig[pos * stride], the lane's slot of a shared
+// array): the 8-word scalar and its carry are not live during the additions (k_verify, NW_DIG_LDS).
+template <int W, bool FIRST, bool FUSED>
+__device__ __forceinline__ void comb_pass_dig(ge_p3& P, const int* dig, int stride, const uint32_t* __restrict__ tab,
+                                              bool neg_pos) {
+    int d = dig[0];
+    ent30 cur = load_ent30(tab + (size_t)(d < 0 ? -d : d) * PRECOMP_WORDS);
+    int pos = 0;
+    if constexpr (FIRST) {
+        const ge_precomp q0 = ent30_precomp(cur);
+        const bool neg0 = neg_pos ? d > 0 : d < 0;
+        d = dig[stride];
+        cur = load_ent30(tab + ((size_t)comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
+        P = ge_from_precomp(ge_precomp_cneg(q0, neg0));
+        pos = 1;
+    }
+#pragma nounroll
+    for (; pos < comb_pos(W); ++pos) {
+        int dn = 0;
+        ent30 nxt;
+        if (pos + 1 < comb_pos(W)) {
+            dn = dig[(pos + 1) * stride];
+            nxt = load_ent30(tab + ((size_t)(pos + 1) * comb_ent(W) + (dn < 0 ? -dn : dn)) * PRECOMP_WORDS);
+        }
+        P = ge_madd<FUSED>(P, ge_precomp_cneg(ent30_precomp(cur), neg_pos ? d > 0 : d < 0));
+        cur = nxt;
+        d = dn;
+    }
+}
+
 // P = s B - h A: radix-2^WB comb over the basepoint table, then radix-2^WA comb over the key
 // table (WA = 0: s B only).  Each step is one gather + one mixed addition, no doublings.
 template <int WB, int WA, bool FUSED = false>

@@ -66,7 +66,7 @@ NW_HD ge_precomp ge_precomp_identity() {
 }
 
 #ifndef NW_MADD3
-#define NW_MADD3 0
+#define NW_MADD3 1   // with NW_DIG_LDS (k_verify): a, b, c as one three-way fused group
 #endif
 #if NW_HALF_NIELS
 // p + q (mixed, halved entry).  The HWCD formulas with every quantity halved: A/2 = (Y1-X1)(y-x)/2,
@@ -97,7 +97,8 @@ NW_HD madd_mid ge_madd_s1(const ge_p3& p, const ge_precomp& q) {
         m.f = fe_sub2p_loose(p.Z, c);
         m.g = fe_add(p.Z, c);
     } else if constexpr (FUSED) {
-        // a and b as one interleaved pair; c alone by operand scanning (a lone fused chain stalls)
+        // a and b as one interleaved pair; c alone by operand scanning (a lone fused chain stalls);
+        // used when the three-way group does not fit the register budget
         fe a, b;
         fe_mul2(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx);
         const fe c = fe_mul(p.T, q.xy2d);

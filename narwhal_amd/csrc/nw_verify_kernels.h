@@ -46,8 +46,8 @@ __device__ __forceinline__ void coeff_z(const VerifyParams& a, uint32_t i, uint3
 // Occupancy: the 32-byte-digest kernel (certificates, votes, headers: the hot path) is held to
 // 168 VGPRs = 3 waves per SIMD (a few spills, measured faster than 2 waves at 169-175 VGPRs).
 // The generic-message kernel (worker chunks) is left unbounded: bounding it spills heavily.
-#ifndef NW_H_LDS
-#define NW_H_LDS 0
+#ifndef NW_DIG_LDS
+#define NW_DIG_LDS 1   // digits precomputed into LDS (0: consumed from the scalar in the loop)
 #endif
 #ifndef NW_VERIFY_WAVES
 #define NW_VERIFY_WAVES 3
@@ -71,25 +71,26 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     }
     uint32_t* frow = a.pbuf + (size_t)PREC_FLAGS_ROW * a.n;
     frow[gid] = flags;   // parked (coalesced) so neither flags nor i stays live through the combs
-#if NW_H_LDS
-    // h parked in LDS through the basepoint pass (8 VGPRs fewer at the loop's peak)
-    __shared__ uint32_t h_park[8][256];
+#if NW_DIG_LDS
+    // every signed digit of s and h computed up front into LDS: neither scalar nor the digit carry
+    // is live during the comb additions (register room for a three-product first group, NW_MADD3)
+    constexpr int NB = comb_pos(B_WINDOW), NA = comb_pos(WA);
+    __shared__ int digs[(NB + NA) * 256];
+    {
+        uint32_t sc[8];
+        int carry = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) h_park[k][threadIdx.x] = h[k];
+        for (int k = 0; k < 8; ++k) sc[k] = sok ? S[k] : 0u;
+#pragma unroll
+        for (int p = 0; p < NB; ++p) digs[p * 256 + threadIdx.x] = next_digit<B_WINDOW>(sc, carry);
+        carry = 0;
+#pragma unroll
+        for (int p = 0; p < NA; ++p) digs[(NB + p) * 256 + threadIdx.x] = next_digit<WA>(h, carry);
+    }
     ge_p3 P;
-    {
-        uint32_t s_use[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s_use[k] = sok ? S[k] : 0u;
-        comb_pass<B_WINDOW, true, MSGMODE == 0 && NW_MADD_FUSED>(P, s_use, a.btab, false);
-    }
-    asm volatile("" ::: "memory");
-    {
-        uint32_t h2[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) h2[k] = h_park[k][threadIdx.x];
-        comb_pass<WA, false, MSGMODE == 0 && NW_MADD_FUSED>(P, h2, a.key_tab + (size_t)slot * comb_words(WA), true);
-    }
+    comb_pass_dig<B_WINDOW, true, MSGMODE == 0 && NW_MADD_FUSED>(P, digs + threadIdx.x, 256, a.btab, false);
+    comb_pass_dig<WA, false, MSGMODE == 0 && NW_MADD_FUSED>(P, digs + NB * 256 + threadIdx.x, 256,
+                                                           a.key_tab + (size_t)slot * comb_words(WA), true);
 #else
     // fused-carry products only in the 3-waves-per-SIMD kernel (MSGMODE 0); see ge_madd_s1
     const ge_p3 P = compute_P<WA, B_WINDOW, MSGMODE == 0 && NW_MADD_FUSED>(S, h, sok, a.btab,
