@@ -162,7 +162,13 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
 // exact remaining batch sum (usually empty) must be the identity.  One 64-lane wave per
 // certificate: lanes stride over the votes (coalesced flag reads), wave reductions combine them;
 // the exact sum over slow-path terms (failing certificates only) is a lane-strided sum + shuffle tree.
-__global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
+// Occupancy bound: the common path (flag reduction, stake sum) needs few registers, the rare exact
+// sum over failing votes (ge_add chain) many; bounding the kernel to 8 waves per SIMD (64 VGPRs)
+// lets the rare path spill instead of capping every certificate's wave at 3 per SIMD.
+#ifndef NW_FINALIZE_WAVES
+#define NW_FINALIZE_WAVES 8
+#endif
+__global__ void __launch_bounds__(256, NW_FINALIZE_WAVES) k_cert_finalize(FinalizeParams a) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (a.sig_ok) {   // strict verdict bytes of every signature (the flags are final here)
