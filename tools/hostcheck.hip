@@ -124,6 +124,34 @@ void hc_point_ops(const uint8_t* a, const uint8_t* b, const uint8_t* k, uint8_t*
     w2b(kmul, o);
 }
 
+// The fused-carry products of k_verify's mixed addition (ge_madd<true>: fe_mul3 + fe_mul4_efgh),
+// and the pair / triple / quad product groups against fe_mul on the same operands.
+// out: compress(a + precomp(b)) by ge_madd<true>; returns 1 iff every grouped product equals fe_mul.
+int hc_madd_fused(const uint8_t* a, const uint8_t* b, uint8_t* madd) {
+    uint32_t wa[8], wb[8], o[8];
+    b2w(wa, a);
+    b2w(wb, b);
+    ge_p3 pa, pb;
+    ge_decompress(pa, wa);
+    ge_decompress(pb, wb);
+    const ge_precomp q = ge_precomp_cneg(ge_to_precomp(pb), false);
+    ge_compress_w(o, ge_madd<true>(pa, q));
+    w2b(madd, o);
+    // loose operands as the addition produces them (k = 5 first operands, k <= 3 second operands)
+    const fe f1 = fe_sub_loose(pa.Y, pa.X), f2 = fe_add(pa.Y, pa.X), f3 = pa.T;
+    const fe g1 = q.ymx, g2 = q.ypx, g3 = fe_sub2p_loose(pa.Z, q.xy2d);
+    fe h1, h2, h3, x, y, z, t;
+    bool ok = true;
+    auto same = [](const fe& u, const fe& v) { return fe_iszero(fe_sub(u, v)); };
+    fe_mul2(h1, f1, g1, h2, f2, g2);
+    ok = ok && same(h1, fe_mul(f1, g1)) && same(h2, fe_mul(f2, g2));
+    fe_mul3(h1, f1, g1, h2, f2, g2, h3, f3, g3);
+    ok = ok && same(h1, fe_mul(f1, g1)) && same(h2, fe_mul(f2, g2)) && same(h3, fe_mul(f3, g3));
+    fe_mul4_efgh(x, y, z, t, f1, g3, f2, g2);   // e f, g h, g f, e h
+    ok = ok && same(x, fe_mul(f1, g3)) && same(y, fe_mul(f2, g2)) && same(z, fe_mul(f2, g3)) && same(t, fe_mul(f1, g2));
+    return ok ? 1 : 0;
+}
+
 // Build the comb table of one key exactly as k_key_prep + k_comb_entries do.
 uint32_t hc_build_comb(const uint8_t* key, uint32_t* tab, int w) {
     uint32_t raw[8];

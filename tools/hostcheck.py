@@ -100,6 +100,9 @@ def check_points(rng, n):
         assert outs[1].raw == o.pt_compress(o.pt_double(A)), "dbl"
         assert outs[2].raw == o.pt_compress(o.pt_add(A, Bp)), "madd"
         assert outs[3].raw == o.pt_compress(o.pt_mul(k, A)), "kmul"
+        fused = ctypes.create_string_buffer(32)
+        assert lib.hc_madd_fused(ea, eb, fused) == 1, "fused product groups"
+        assert fused.raw == o.pt_compress(o.pt_add(A, Bp)), "madd (fused-carry products)"
     # decompression incl. non-canonical / invalid encodings
     cases = [bytes(32), b32(1), b32(P), b32(P + 1), b32(P + 18), b32((1 << 255) - 1),
              b32(1 | (1 << 255)), b32(P | (1 << 255))]
