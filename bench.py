@@ -29,6 +29,7 @@ Prints ONE JSON line (rank 0):
 """
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -54,10 +55,13 @@ def comb_pos(w):
 
 
 def kverify_fm_per_sig(key_window, base_window=B_WINDOW):
-    """k_verify's field multiplications per signature: one mixed addition per comb digit position
-    of s (basepoint comb) and of h (key comb); no doublings (nw_core.h comb_sB_minus_hA).  The
-    SHA-512 block, mod-l reduction and digit recoding are VALU work not counted here."""
-    return MADD_FM * (comb_pos(base_window) + comb_pos(key_window))
+    """k_verify's field multiplications per signature, as the kernel executes them: one mixed
+    addition per comb digit position of s (basepoint comb) and of h (key comb), no doublings,
+    except the chain's first entry, which is converted to extended coordinates with ONE
+    multiplication (T = X*Y) instead of being added to the identity (nw_core.h comb_pass_dig<...,
+    true, ...>).  C2 (W24 + W20): 7 x (11 + 13 - 1) + 1 = 162.  The SHA-512 block, mod-l reduction
+    and digit recoding are VALU work not counted here."""
+    return MADD_FM * (comb_pos(base_window) + comb_pos(key_window) - 1) + 1
 
 
 def valu_peak_mad_per_s():
@@ -106,37 +110,63 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline(cs, com, seconds):
+def cpu_thread_candidates():
+    """Thread counts worth timing: the cgroup quota and twice it (a quota of q CPUs still lets 2q
+    threads overlap their stalls; beyond that they only time-slice), capped by the affinity mask.
+    Without a quota: the affinity count."""
+    aff = host_cores()
+    q = cgroup_cpu_quota()
+    if not q:
+        return [aff]
+    base = max(1, int(math.ceil(q)))
+    return sorted({min(aff, base), min(aff, 2 * base)})
+
+
+def cpu_baseline(cs, com, seconds, probe_seconds=2.5, label="C2"):
     """Oracle restatement timed on the host cores (rank 0, N = 1 only): bounded sample of
-    certificates.  Default thread count = every core in this process's affinity mask."""
+    certificates.  A short sweep over the candidate thread counts (cpu_thread_candidates; forced
+    with NW_CPU_THREADS) picks the host's best rate, which is then timed on the main sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import nw_ref   # C restatement of dalek's u64 backend (oracle/nw_ref.c); test/baseline only
-    threads = int(os.environ.get("NW_CPU_THREADS", "0")) or host_cores()
     zseed = bytes(32)
-    done_sigs = done_certs = 0
-    per_call = max(64, 4 * threads)
-    c = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        sel = [(c + k) % cs.ncerts for k in range(per_call)]
-        ok = nw_ref.verify_certs(cs, com, sel, zseed, threads)
-        assert all(ok), "CPU baseline rejected an honest certificate"
-        done_certs += len(sel)
-        done_sigs += int(sum(int(cs.cert_n[x]) for x in sel))
-        c += per_call
-    dt = time.perf_counter() - t0
-    rate = done_sigs / dt
+    forced = int(os.environ.get("NW_CPU_THREADS", "0"))
+    cands = [forced] if forced else cpu_thread_candidates()
+
+    def run(threads, secs):
+        done_sigs = done_certs = 0
+        per_call = max(64, 4 * threads)
+        c = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < secs:
+            sel = [(c + k) % cs.ncerts for k in range(per_call)]
+            ok = nw_ref.verify_certs(cs, com, sel, zseed, threads)
+            assert all(ok), "CPU baseline rejected an honest certificate"
+            done_certs += len(sel)
+            done_sigs += int(sum(int(cs.cert_n[x]) for x in sel))
+            c += per_call
+        dt = time.perf_counter() - t0
+        return done_sigs / dt, done_sigs, done_certs, dt
+
+    sweep = {}
+    if len(cands) > 1:
+        for t in cands:
+            sweep[str(t)] = run(t, probe_seconds)[0]
+        threads = max(cands, key=lambda t: sweep[str(t)])
+    else:
+        threads = cands[0]
+    rate, done_sigs, done_certs, dt = run(threads, seconds)
     return {"value": rate, "unit": "sigs/s", "cores": threads, "kind": "port",
             "per_gpu_share": {"value": rate / GPUS_PER_NODE, "cores": threads / GPUS_PER_NODE,
                               "note": "host rate / %d GPUs per node" % GPUS_PER_NODE},
             "cpu_model": cpu_model(),
             # the affinity mask can be far wider than the cgroup's CPU quota (GPU box: 256 vs 16);
-            # threads beyond the quota time-slice, tools/cpu_probe.py -> profiles/r02/cpu_probe_r02.json
-            "cgroup_cpu_quota": cgroup_cpu_quota(),
-            "sample": "%d certificates x %d votes of the C2 workload (%d sigs) in %.1f s on %d threads; "
-                      "oracle/nw_ref.c (C restatement of ed25519-dalek 1.0.1 u64 backend: per-vote A "
+            # threads beyond ~2x the quota only time-slice (profiles/r02/cpu_probe_r02.json)
+            "cgroup_cpu_quota": cgroup_cpu_quota(), "affinity_cpus": host_cores(),
+            "thread_sweep_sigs_per_s": sweep or None,
+            "sample": "%d certificates x %d votes of the %s workload (%d sigs) in %.1f s on %d threads (best of the "
+                      "sweep); oracle/nw_ref.c (C restatement of ed25519-dalek 1.0.1 u64 backend: per-vote A "
                       "decompression + Straus MSM, as crypto/src/lib.rs:206-219)"
-                      % (done_certs, int(cs.cert_n[0]), done_sigs, dt, threads)}
+                      % (done_certs, int(cs.cert_n[0]), label, done_sigs, dt, threads)}
 
 
 def host_fed(eng, cs, slots, zseed, chunks=8, threads=4, reps=5):
@@ -280,7 +310,7 @@ def digest_leg(eng, dev, n_node, n_share, reps, cpu_seconds, verify_step):
                             "note": "peak = k_sha512_many on 2^21 x 1 KiB messages (saturated SHA-512 VALU rate)"}
     del d_small, q_off, q_len, q_out
     if cpu_seconds > 0:
-        threads = host_cores()
+        threads = max(cpu_thread_candidates())
         stop = time.perf_counter() + cpu_seconds
 
         def hash_loop(k):
@@ -336,20 +366,39 @@ def launch_ranks(args, argv):
     return subprocess.call(cmd, env=env)
 
 
+# BASELINE.json configs a bench run can execute on N ranks (one process per GPU).  "rank" scope:
+# the shape is per GPU (weak scaling: C2 = configs[1]; C4 = configs[3], one GPU's eighth of a
+# 10,000-validator node round plus the rank's worker-batch digests).  "node" scope: the shape is
+# the node's round, partitioned over the ranks by shard.partition (strong scaling: C3 =
+# configs[2], 1,000 certificates x 667 votes; config/src/lib.rs:189-194 gives the 2f+1 = 667).
+CONFIGS = {
+    "C2": {"validators": 100, "certs": 14926, "votes": 67, "scope": "rank", "digest_batches": 0,
+           "baseline": "configs[1]: 100-validator committee, 67-vote certificates, 1M signatures per MI355X"},
+    "C3": {"validators": 1000, "certs": 1000, "votes": 667, "scope": "node", "digest_batches": 0,
+           "baseline": "configs[2]: 1,000-validator committee, 667-vote certificates, sharded over the GPUs "
+                       "with an RCCL verdict all-gather"},
+    "C4": {"validators": 10000, "certs": 1250, "votes": 6667, "scope": "rank", "digest_batches": 1250,
+           "baseline": "configs[3]: 10,000-validator committee, 6,667-vote certificates plus worker 500 KB batch "
+                       "SHA-512 digests; per GPU 1/8 of a node round (1,250 certificates, 1,250 batches)"},
+}
+
+
 def parse_args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--validators", type=int, default=100)
-    ap.add_argument("--certs", type=int, default=14926)
-    ap.add_argument("--votes", type=int, default=67)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
+                    help="BASELINE config of the timed step (default C2, the headline)")
+    ap.add_argument("--validators", type=int, default=None, help="override the config's committee size")
+    ap.add_argument("--certs", type=int, default=None, help="override the config's certificate count")
+    ap.add_argument("--votes", type=int, default=None, help="override the config's votes per certificate")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--latency-samples", type=int, default=200)
     ap.add_argument("--digest-batches", type=int, default=10000, help="0 disables the digest leg")
     ap.add_argument("--digest-share", type=int, default=1250, help="C4 per-GPU batch share")
-    ap.add_argument("--no-extras", action="store_true", help="headline only (no host_fed / msm legs)")
+    ap.add_argument("--no-extras", action="store_true", help="headline only (no host_fed / msm / latency legs)")
     ap.add_argument("--key-window", type=int, default=-1,
                     help="key comb window; -1 = committee mode (library sizes it for the loaded committee)")
     ap.add_argument("--dry-run", action="store_true",
@@ -357,9 +406,30 @@ def parse_args(argv):
     return ap.parse_args(argv)
 
 
+def config_plan(args, world, rank):
+    """The rank's share of the configured step (pure host logic; the dry run prints it)."""
+    from narwhal_amd import shard
+    c = dict(CONFIGS[args.config])
+    validators = args.validators or c["validators"]
+    certs = args.certs or c["certs"]
+    votes = args.votes or c["votes"]
+    if c["scope"] == "node":
+        ranges = shard.partition([votes] * certs, world)
+        scaling = "strong"
+    else:
+        ranges = [(r * certs, (r + 1) * certs) for r in range(world)]
+        scaling = "weak"
+    c0, c1 = ranges[rank]
+    return {"config": args.config, "validators": validators, "votes": votes, "node_certs": ranges[-1][1],
+            "ranges": ranges, "first_cert": c0, "ncerts": c1 - c0, "sigs": (c1 - c0) * votes,
+            "total_sigs": ranges[-1][1] * votes, "digest_batches": c["digest_batches"], "scaling": scaling,
+            "baseline": c["baseline"]}
+
+
 def dry_run(args):
     """Rank plumbing of ``--gpus N`` on CPU (tests/test_bench_launch.py): one gloo all_gather of
-    the rank ids, the same barrier/max-over-ranks pattern as the timed loop, one JSON line."""
+    the rank ids and of each rank's workload plan, the same barrier/max-over-ranks pattern as the
+    timed loop, one JSON line."""
     import torch
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -367,22 +437,111 @@ def dry_run(args):
     if world > 1:
         dist.init_process_group("gloo")
     t0 = time.perf_counter()
-    ids = torch.tensor([rank], dtype=torch.int64)
-    got = [torch.zeros(1, dtype=torch.int64) for _ in range(world)]
+    plan = config_plan(args, world, rank)
+    mine = torch.tensor([rank, plan["first_cert"], plan["ncerts"], plan["sigs"], plan["digest_batches"]],
+                        dtype=torch.int64)
+    got = [torch.zeros(5, dtype=torch.int64) for _ in range(world)]
     if world > 1:
-        dist.all_gather(got, ids)
+        dist.all_gather(got, mine)
         el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     else:
-        got = [ids]
+        got = [mine]
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_arg": args.gpus,
-                          "ranks": [int(g.item()) for g in got],
+        print(json.dumps({"dry_run": True, "n_gpus": world, "gpus_arg": args.gpus, "config": args.config,
+                          "ranks": [int(g[0].item()) for g in got],
+                          "shards": [{"first_cert": int(g[1]), "ncerts": int(g[2]), "sigs": int(g[3]),
+                                      "digest_batches": int(g[4])} for g in got],
+                          "total_sigs": plan["total_sigs"], "scaling": plan["scaling"],
                           "local_ranks_env": os.environ.get("LOCAL_RANK")}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def timeit_once(fn):
+    t0 = time.perf_counter()
+    fn()
+    return time.perf_counter() - t0
+
+
+def latency_legs(eng, com, slots, cs, samples):
+    """One-call latencies of the paths the Rust shim calls, host buffers, the
+    call marshalled once so only the ABI call is timed:
+      * strict: crypto::Signature::verify (crypto/src/lib.rs:200-204) -> nw_verify_strict, one
+        header/vote signature (primary/src/core.rs:313,335), key in the committee cache and not;
+      * batch: crypto::Signature::verify_batch (crypto/src/lib.rs:206-219) -> nw_verify_batch, one
+        2f+1 certificate at 67 / 667 / 6,667 votes (committee cached), and 67 votes with keys
+        outside the cache (Pippenger MSM)."""
+    import numpy as np
+    from narwhal_amd import _lib, workload
+
+    def p50(fn, n):
+        for _ in range(5):
+            fn()
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return {"p50_ms": ts[len(ts) // 2] * 1e3, "p99_ms": ts[int(len(ts) * 0.99)] * 1e3, "min_ms": ts[0] * 1e3,
+                "samples": n}
+
+    out = {}
+    msg, pk, sig = bytes(cs.msgs[0]), bytes(com.pks[cs.signer[0]]), bytes(cs.sigs[0])
+    assert eng.verify_strict(msg, pk, sig)
+    out["strict_cached"] = p50(lambda: eng.verify_strict(msg, pk, sig), samples)
+    fseed = np.frombuffer(os.urandom(32), np.uint8).reshape(1, 32)
+    fpk, fsig = eng.sign_many_np(fseed, np.frombuffer(msg, np.uint8).reshape(1, 32))
+    fpk, fsig = bytes(fpk[0]), bytes(fsig[0])
+    assert eng.verify_strict(msg, fpk, fsig)
+    out["strict_uncached"] = p50(lambda: eng.verify_strict(msg, fpk, fsig), samples)
+
+    def cert_call(e, c_com, c_cs, c):
+        f, n = int(c_cs.cert_first[c]), int(c_cs.cert_n[c])
+        m = bytes(c_cs.msgs[c])
+        return e.prepare_batch_call([m] * n, [bytes(c_com.pks[k]) for k in c_cs.signer[f:f + n]],
+                                    [bytes(x) for x in c_cs.sigs[f:f + n]])
+
+    zseed = os.urandom(32)
+    call = cert_call(eng, com, cs, 0)
+    assert call(zseed, 0)
+    out["batch_cached_%d" % int(cs.cert_n[0])] = p50(lambda: call(zseed, 0), samples)
+    # keys outside the cache: a fresh committee of the same size that is never loaded
+    nu = int(cs.cert_n[0])
+    useeds = np.frombuffer(os.urandom(32 * nu), np.uint8).reshape(nu, 32).copy()
+    ucom = workload.Committee(seeds=useeds, pks=eng.sign_many_np(useeds, np.zeros((nu, 32), np.uint8))[0],
+                              stake=np.ones(nu, np.uint32))
+    ucs = workload.make_certificates(ucom, 2, ucom.size, eng)
+    ucall = cert_call(eng, ucom, ucs, 0)
+    assert ucall(zseed, 0)
+    out["batch_uncached_%d" % ucom.size] = p50(lambda: ucall(zseed, 0), samples)
+    # Header::verify's id check at N = 10,000: one SHA-512 of a 6,667-parent header preimage
+    # (author 32 + round 8 + 6,667 x 32 B = 213,384 B, primary/src/messages.rs:50,71-83)
+    import hashlib
+    pre = os.urandom(32 + 8 + 6667 * 32)
+    assert eng.sha512(pre) == hashlib.sha512(pre).digest()
+    out["header_digest_6667_parents"] = dict(p50(lambda: eng.sha512(pre), max(20, samples // 4)),
+                                             bytes=len(pre),
+                                             hashlib_1core_ms=min(timeit_once(lambda: hashlib.sha512(pre).digest())
+                                                                  for _ in range(20)) * 1e3)
+    for nval in (1000, 10000):
+        e2 = _lib.Engine(device=eng.device, key_window=-1)
+        c2 = workload.make_committee(nval, e2)
+        e2.committee_load_np(c2.pks, c2.stake)
+        votes = 2 * nval // 3 + 1
+        k_cs = workload.make_certificates(c2, 2, votes, e2)
+        kc = cert_call(e2, c2, k_cs, 0)
+        assert kc(zseed, 0)
+        out["batch_cached_%d" % votes] = dict(p50(lambda: kc(zseed, 0), max(20, samples // 4)),
+                                              key_window=e2.key_window())
+        del kc
+        e2.close()
+    out["note"] = ("host buffers, one ABI call per sample (marshalled once); cached = keys in the committee key "
+                   "cache (nw_committee_load at spawn), uncached = variable-base path (k_verify_var / MSM)")
+    return out
 
 
 def main(argv=None):
@@ -408,11 +567,13 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from narwhal_amd import _lib, workload
+    plan = config_plan(args, world, rank)
     eng = _lib.Engine(device=local, key_window=args.key_window)
-    com = workload.make_committee(args.validators, eng)
+    com = workload.make_committee(plan["validators"], eng)
     slots = eng.committee_load_np(com.pks, com.stake)
-    first_cert = rank * args.certs                      # each rank: its own shard of certificates
-    cs = workload.make_certificates(com, args.certs, args.votes, eng, first_cert=first_cert)
+    first_cert = plan["first_cert"]                     # each rank: its own shard of certificates
+    cs = workload.make_certificates(com, plan["ncerts"], plan["votes"], eng, first_cert=first_cert)
+    ranges = plan["ranges"]                             # node-wide certificate ranges
 
     dev = torch.device("cuda", local)
     d_sig = torch.from_numpy(cs.sigs).to(dev)
@@ -424,7 +585,6 @@ def main(argv=None):
     d_flags = torch.zeros(cs.nsigs, dtype=torch.int32, device=dev)
     d_stake = torch.zeros(cs.ncerts, dtype=torch.int64, device=dev)
     d_status = torch.zeros(1, dtype=torch.int32, device=dev)   # asynchronous input check (NW_OK / NW_ERR_ARG)
-    ranges = [(r * args.certs, (r + 1) * args.certs) for r in range(world)]   # node-wide certificate ranges
     zseed = os.urandom(32)
 
     def verify_step(stream):
@@ -432,15 +592,41 @@ def main(argv=None):
                              d_signer.data_ptr(), d_msg.data_ptr(), zseed, first_cert, d_ok.data_ptr(),
                              d_flags.data_ptr(), d_stake.data_ptr(), stream.cuda_stream, d_status=d_status.data_ptr())
 
+    # C4: the rank's worker-batch digests (worker/src/processor.rs:65) run inside the timed step on
+    # a second stream, concurrently with the verify kernels; the step ends when both are done
+    ndig = plan["digest_batches"]
+    if ndig:
+        import hashlib
+        host_b = workload.worker_batches_np(ndig)
+        blen = host_b.shape[1]
+        d_bdata = torch.from_numpy(host_b.reshape(-1)).to(dev)
+        d_boff = torch.arange(ndig, dtype=torch.int64, device=dev) * blen
+        d_blen = torch.full((ndig,), blen, dtype=torch.int64, device=dev)
+        d_bout = torch.empty((ndig, 64), dtype=torch.uint8, device=dev)
+        s_dig = torch.cuda.Stream(device=dev)
+        ev_dig = torch.cuda.Event()
+
     def step():
-        verify_step(torch.cuda.current_stream())
+        cur = torch.cuda.current_stream()
+        if ndig:
+            s_dig.wait_stream(cur)
+            eng.sha512_many_dev(d_bdata.data_ptr(), d_boff.data_ptr(), d_blen.data_ptr(), ndig, d_bout.data_ptr(),
+                                s_dig.cuda_stream)
+            ev_dig.record(s_dig)
+        verify_step(cur)
+        if ndig:
+            cur.wait_event(ev_dig)
         if world > 1:
             shard.allgather_verdicts(d_ok, d_stake, ranges)   # RCCL all_gather of bitmaps + stake
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ok_all = bool(d_ok.all().item()) and bool((d_stake == args.votes).all().item()) and int(d_status.item()) == 0
+    ok_all = (bool(d_ok.all().item()) and bool((d_stake == plan["votes"]).all().item())
+              and int(d_status.item()) == 0)
+    if ndig:
+        for b in (0, ndig - 1):
+            ok_all = ok_all and bytes(d_bout[b].cpu().numpy()) == hashlib.sha512(host_b[b].tobytes()).digest()
     if world > 1:
         dist.barrier()
     eng.profile_read()             # discard warmup events
@@ -464,9 +650,9 @@ def main(argv=None):
         okt = torch.tensor([1 if ok_all else 0], dtype=torch.int32, device=dev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok_all = bool(okt.item())
-    assert ok_all, "honest workload rejected"
+    assert ok_all, "honest workload rejected (or a worker-batch digest mismatched)"
 
-    total_sigs = world * cs.nsigs * args.steps
+    total_sigs = plan["total_sigs"] * args.steps       # every rank's signatures (node-wide)
     value = total_sigs / elapsed
 
     if rank == 0:
@@ -479,14 +665,15 @@ def main(argv=None):
         fm = kverify_fm_per_sig(kw, bw)
         peak = valu_peak_mad_per_s() / 1e12
         achieved = sigs_per_launch * fm * MADS_PER_FM / avg_launch_s / 1e12
-        v1 = COST_MODEL_V1_FM.get(args.votes)
+        v1 = COST_MODEL_V1_FM.get(plan["votes"])
         roofline = {
             "bound": "valu", "kernel": "k_verify", "achieved": achieved, "peak": peak, "unit": "TMAD/s",
-            "frac": achieved / peak, "traffic": traffic_per_launch(),
+            "frac": achieved / peak,
+            "traffic": traffic_per_launch() if args.config == "C2" else None,
             "avg_launch_ms": avg_launch_s * 1e3, "launches": kn,
             "work_model": "%.0f sigs/launch (%d launches per step) x %d FM/sig (7 FM per mixed addition x (%d basepoint "
-                          "+ %d key) comb positions, key window %d) x 100 u32 MADs; SHA-512/mod-l/recoding VALU work "
-                          "not counted; peak = measured v_mad_u64_u32 rate"
+                          "+ %d key - 1) comb positions + 1 FM for the chain's first entry, key window %d) x 100 u32 "
+                          "MADs; SHA-512/mod-l/recoding VALU work not counted; peak = measured v_mad_u64_u32 rate"
                           % (sigs_per_launch, kn // args.steps, fm, comb_pos(bw), comb_pos(kw), kw),
             "dalek_equiv": {"fm_per_sig": v1, "TMADps": (sigs_per_launch * v1 * MADS_PER_FM / avg_launch_s / 1e12)
                             if v1 else None,
@@ -504,30 +691,41 @@ def main(argv=None):
             lat.append(time.perf_counter() - t1)
             assert cok[0] == 1
         lat.sort()
+        strong = plan["scaling"] == "strong"
+        workload_desc = ("%s: %d-validator committee, %d certificates x %d votes (%d sigs) %s"
+                         % (args.config, plan["validators"], plan["node_certs"] if strong else plan["ncerts"],
+                            plan["votes"], plan["total_sigs"] if strong else cs.nsigs,
+                            "per node round, partitioned over the GPUs" if strong else "per GPU"))
+        if ndig:
+            workload_desc += " + %d worker-batch SHA-512 digests (%d B each) per GPU on a second stream" % (ndig, blen)
         out = {
             "metric": METRIC, "value": value, "unit": "sigs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "scaling": plan["scaling"], "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (GPU-signed RFC 8032 signatures over SHA-512 certificate digests)",
-            "config": {"workload": "C2: %d-validator committee, %d certificates x %d votes (%d sigs) per GPU"
-                                   % (args.validators, args.certs, args.votes, cs.nsigs),
-                       "validators": args.validators, "certs_per_gpu": args.certs, "votes_per_cert": args.votes,
+            "config": {"workload": workload_desc, "baseline_config": plan["baseline"],
+                       "validators": plan["validators"], "certs_per_gpu": cs.ncerts, "votes_per_cert": plan["votes"],
                        "key_window": kw,
                        "parallelism": "certificate shards per GPU; RCCL all_gather of verdict bitmaps + stake"},
             "p50_cert_latency_ms": lat[len(lat) // 2] * 1e3 if lat else None,
             "p99_cert_latency_ms": lat[int(len(lat) * 0.99)] * 1e3 if lat else None,
             "roofline": roofline,
         }
+        if ndig:
+            out["digest_in_step"] = {"batches_per_gpu": ndig, "bytes_per_gpu_per_step": ndig * blen,
+                                     "GBps_per_gpu": ndig * blen * args.steps / elapsed / 1e9}
         # GPU legs first: the CPU baselines run more threads than the container's CPU quota, and the
         # cgroup throttling that follows would slow the host side of the next leg
-        if world == 1 and not args.no_extras:
+        c2 = args.config == "C2"
+        if world == 1 and c2 and not args.no_extras:
             out["host_fed"] = host_fed(eng, cs, slots, zseed)
             out["msm"] = msm_leg(eng)
-        if world == 1 and args.digest_batches > 0:
+            out["latency"] = latency_legs(eng, com, slots, cs, args.latency_samples)
+        if world == 1 and c2 and args.digest_batches > 0:
             out["digest"] = digest_leg(eng, dev, args.digest_batches, args.digest_share, 3,
                                        0.0 if args.no_cpu_baseline else 3.0, verify_step)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cs, com, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(cs, com, args.cpu_seconds, label=args.config)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

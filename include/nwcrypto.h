@@ -43,6 +43,12 @@ extern "C" {
 #define NW_ERR_DEVICE 3
 #define NW_ERR_NOMEM 4
 
+/* ABI revision of this header.  2: nw_verify_certs_dev gained ``d_status`` before ``stream`` and
+ * every batch entry point rejects a NULL zseed (revision 1 = nwcrypto 0.1).  The shared library's
+ * soname carries it (libnwcrypto.so.2), so a caller built against revision 1 does not load this
+ * library by accident; callers may also compare nw_abi_version() with NW_ABI_VERSION at startup. */
+#define NW_ABI_VERSION 2
+
 /* Per-signature flag bits written by the verify kernels (nw_verify_certs sig_flags output). */
 #define NW_F_S_OK 0x001u      /* S < l (ed25519 high-bit check + dalek check_scalar) */
 #define NW_F_A_OK 0x002u      /* public key decodes (dalek::PublicKey::from_bytes) */
@@ -94,7 +100,8 @@ int nw_committee_load(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stak
                       uint32_t* slot_out);
 /* Number of cached keys. */
 size_t nw_committee_size(const nw_ctx* ctx);
-/* Key comb window in use (8 / 12 / 16; 0 before the first load). */
+/* Key comb window in use (8 / 12 / 16 / 20; 0 before the first load, or -1 while committee mode
+ * has not sized it yet). */
 int nw_key_window(const nw_ctx* ctx);
 /* Basepoint comb window this library was built with (additions per s*B = ceil(256 / w)). */
 int nw_base_window(void);
@@ -279,6 +286,8 @@ int nw_certificates_verify(nw_ctx* ctx, const nw_committee* committee, const uin
 
 /* Library build identifier (gfx target, build date). */
 const char* nw_version(void);
+/* NW_ABI_VERSION the library was built with. */
+int nw_abi_version(void);
 
 #ifdef __cplusplus
 }

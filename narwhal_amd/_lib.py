@@ -56,7 +56,9 @@ DAG_PENDING, DAG_OK, DAG_INVALID_SIGNATURE, DAG_SERIALIZATION, DAG_INVALID_HEADE
 DAG_MALFORMED_HEADER, DAG_UNKNOWN_AUTHORITY, DAG_AUTHORITY_REUSE, DAG_REQUIRES_QUORUM = 4, 5, 6, 7
 DAG_NOT_CERTIFICATE = 8
 
-_OPTIONAL = {"nw_profile_read_sigs", "nw_base_window", "nw_cert_batch_decode", "nw_cert_batch_size",
+ABI_VERSION = 2    # NW_ABI_VERSION of include/nwcrypto.h this binding is written against
+
+_OPTIONAL = {"nw_abi_version", "nw_profile_read_sigs", "nw_base_window", "nw_cert_batch_decode", "nw_cert_batch_size",
              "nw_cert_batch_view", "nw_cert_batch_free", "nw_cert_batch_verify", "nw_certificates_verify"}
 
 
@@ -92,6 +94,7 @@ def _load() -> ctypes.CDLL:
         "nw_profile_read": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64)]),
         "nw_profile_read_sigs": (I, [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "nw_version": (ctypes.c_char_p, []),
+        "nw_abi_version": (I, []),
         "nw_cert_batch_decode": (I, [ctypes.POINTER(NwCommittee), P, P, S, ctypes.POINTER(P)]),
         "nw_cert_batch_size": (S, [P]),
         "nw_cert_batch_view": (I, [P, S, ctypes.POINTER(NwCertView)]),
@@ -105,6 +108,10 @@ def _load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if LIB_PATH == os.path.join(_HERE, "libnwcrypto.so"):
+        abi = lib.nw_abi_version() if hasattr(lib, "nw_abi_version") else 1
+        if abi != ABI_VERSION:
+            raise ImportError("libnwcrypto.so has ABI %d, this binding expects %d: rebuild it" % (abi, ABI_VERSION))
     return lib
 
 
@@ -388,6 +395,27 @@ class Engine:
                                                _buf(b"".join(map(bytes, sigs))), n, bytes(zseed), batch_index,
                                                z_offset, pt, ctypes.byref(bad)), "nw_verify_batch_partial")
         return pt.raw, bool(bad.value)
+
+    def prepare_batch_call(self, msgs, pks, sigs):
+        """Marshal one nw_verify_batch call once; returns ``call(zseed, batch_index) -> bool`` that
+        only crosses the ABI (latency legs: the cost a Rust caller pays, not Python's packing)."""
+        import numpy as np
+        n = len(sigs)
+        keep = [np.ascontiguousarray(np.frombuffer(b"".join(bytes(m) for m in msgs), np.uint8)),
+                np.ascontiguousarray(np.frombuffer(b"".join(bytes(k) for k in pks), np.uint8)),
+                np.ascontiguousarray(np.frombuffer(b"".join(bytes(s) for s in sigs), np.uint8))]
+        lens = np.array([len(m) for m in msgs], np.uint64)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+        ptrs = (keep[0].ctypes.data + offs).astype(np.uint64)
+        keep += [lens, ptrs]
+        lib, ctx = LIB, self._ctx
+
+        def call(zseed: bytes, batch_index: int = 0) -> bool:
+            _ = keep
+            return self.check(lib.nw_verify_batch(ctx, ptrs.ctypes.data, lens.ctypes.data, keep[1].ctypes.data,
+                                                  keep[2].ctypes.data, n, zseed, batch_index),
+                              "nw_verify_batch") == NW_OK
+        return call
 
     def points_sum_is_identity(self, points) -> bool:
         blob = b"".join(bytes(p) for p in points)

@@ -247,7 +247,9 @@ private:
     bool sync_on_release_ = false;
 };
 
-// Wait for every call that may still read the key tables (exclusive key lock held).
+// Wait for every call that may still read the key tables (exclusive key lock held).  Every lease
+// is taken under the shared key lock, so no lease is live here and nothing else touches
+// pending/done while we read them.
 int drain_all(nw_ctx* ctx) {
     std::lock_guard<std::mutex> g(ctx->pool_mu);
     for (auto& w : ctx->pool)
@@ -389,7 +391,8 @@ int ensure_slots(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, si
         auto it = ctx->slot_of.find(k);
         if (it != ctx->slot_of.end()) {
             slots[i] = it->second;
-            if (stake) refresh.emplace_back(it->second, stake[i]);
+            // only a changed stake is a refresh: an unchanged reload must not drain every in-flight call
+            if (stake && ctx->h_stake[it->second] != stake[i]) refresh.emplace_back(it->second, stake[i]);
             continue;
         }
         auto pit = pending.find(k);
@@ -836,7 +839,9 @@ bool zseed_ok(nw_ctx* ctx, const uint8_t* zseed) {
 
 extern "C" {
 
-const char* nw_version(void) { return "nwcrypto 0.2 gfx950 " __DATE__; }
+const char* nw_version(void) { return "nwcrypto 0.3 gfx950 " __DATE__; }
+
+int nw_abi_version(void) { return NW_ABI_VERSION; }
 
 int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     if (!out) return NW_ERR_ARG;
@@ -1066,6 +1071,8 @@ int nw_verify_batch_partial(nw_ctx* ctx, const uint8_t* const* msg, const size_t
 int nw_points_sum_is_identity(nw_ctx* ctx, const uint8_t (*points)[NW_POINT_BYTES], size_t k, int* is_identity) {
     if (!ctx || !is_identity || (k && !points)) return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    // every lease holds the key lock shared: drain_all (exclusive) then never races a lease
+    std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);
     Lease lease(ctx);
     Workspace* ws = lease.ws();
     if (!ws) return NW_ERR_DEVICE;
@@ -1223,6 +1230,10 @@ int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);
+    if (nsigs && ctx->nkeys == 0) {   // every slot is out of range, and the kernels have no table to clamp to
+        set_error(ctx, "nw_verify_certs_dev: no committee loaded (signer slots outside the empty key cache)");
+        return NW_ERR_ARG;
+    }
     Lease lease(ctx);
     Workspace* ws = lease.ws();
     if (!ws) return NW_ERR_DEVICE;
@@ -1283,6 +1294,7 @@ int nw_sha512_many(nw_ctx* ctx, const uint8_t* base, const uint64_t* off, const 
     std::vector<uint64_t> roff(n);
     for (size_t i = 0; i < n; ++i) roff[i] = off[i] - lo;
     const size_t span = (size_t)(hi - lo);
+    std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);   // see nw_points_sum_is_identity
     Lease lease(ctx);
     Workspace* ws = lease.ws();
     if (!ws) return NW_ERR_DEVICE;
@@ -1329,6 +1341,7 @@ int nw_sign_many(nw_ctx* ctx, const uint8_t (*seed)[32], const uint8_t* msgs, si
     if (n == 0) return NW_OK;
     if (n > 0xFFFFFFF0u) return NW_ERR_ARG;
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);   // see nw_points_sum_is_identity
     Lease lease(ctx);
     Workspace* ws = lease.ws();
     if (!ws) return NW_ERR_DEVICE;

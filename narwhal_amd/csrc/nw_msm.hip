@@ -526,9 +526,15 @@ __global__ void __launch_bounds__(64) k_points_identity(uint32_t npts, const uin
 
 template <int C>
 static hipError_t launch_msm_c(const MsmParams& p, hipStream_t st) {
-    hipLaunchKernelGGL(k_msm_prep<C>, dim3(blocks_for(p.nsig, 256)), dim3(256), 0, st, p);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    // no signatures (an empty shard of a split batch, counts all 0): the bad flags are zeroed by
+    // the metadata upload and no zs column is read, so wsum/final give the identity -> Ok, as
+    // dalek's empty batch
+    if (p.nsig) {
+        hipLaunchKernelGGL(k_msm_prep<C>, dim3(blocks_for(p.nsig, 256)), dim3(256), 0, st, p);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     if (p.ntasks) {
         hipLaunchKernelGGL(k_msm_bucket<C>, dim3(p.ntasks), dim3(64), 0, st, p);
         e = hipGetLastError();

@@ -177,3 +177,49 @@ def test_null_zseed_rejected(setup):
     assert L.nw_verify_batches_pk(h, 1, cnt, m, ln, pk, sg, None, 0, out) == _lib.NW_ERR_ARG
     assert L.nw_verify_certs_dev(h, 0, None, None, 0, None, None, None, None, 0, None, None, None, None,
                                  None) == _lib.NW_ERR_ARG
+
+
+def test_dev_call_before_any_committee_load(setup):
+    """A fixed-window context with an empty key cache: nw_verify_certs_dev is NW_ERR_ARG on the host
+    (every slot is out of range and there is no table to clamp to), synchronous and asynchronous
+    forms alike, and never reaches the GPU."""
+    import torch
+    from narwhal_amd import _lib
+    _, com, slots, cs, dev = setup
+    empty = _lib.Engine(device=0, key_window=16)
+    try:
+        assert empty.committee_size() == 0
+        st = torch.cuda.current_stream()
+        d = _dev_inputs(cs, slots, dev)
+        status = torch.full((1,), 99, dtype=torch.int32, device=dev)
+        for s in (None, status):
+            with pytest.raises(_lib.DeviceError, match="rc=2"):
+                _run_dev(empty, cs, d, dev, st, 0, status=s)
+        torch.cuda.synchronize()
+    finally:
+        empty.close()
+
+
+def test_committee_reload_while_dev_work_in_flight(setup):
+    """nw_committee_load of an already-cached committee with unchanged stakes changes nothing and
+    does not drain in-flight _dev calls; a changed stake is applied after them.  Verdicts of the
+    in-flight calls are unaffected."""
+    import torch
+    eng, com, slots, cs, dev = setup
+    st = torch.cuda.Stream(device=dev)
+    d = _dev_inputs(cs, slots, dev)
+    want = eng.verify_certs_np(cs.cert_first, cs.cert_n, cs.sigs, slots[cs.signer], cs.msgs, ZSEED, 0)
+    outs = []
+    with torch.cuda.stream(st):
+        for _ in range(4):
+            outs.append(_run_dev(eng, cs, d, dev, st, 0))
+    again = eng.committee_load_np(com.pks, com.stake)            # unchanged: no refresh
+    assert (again == slots).all()
+    doubled = eng.committee_load_np(com.pks, com.stake * 2)      # changed: drains, then applies
+    assert (doubled == slots).all()
+    torch.cuda.synchronize()
+    for ok, flags, stake in outs:
+        assert (ok.cpu().numpy() == want[0]).all()
+    r2 = eng.verify_certs_np(cs.cert_first, cs.cert_n, cs.sigs, slots[cs.signer], cs.msgs, ZSEED, 0)
+    assert (r2[2] == 2 * want[2]).all()
+    eng.committee_load_np(com.pks, com.stake)                     # restore for the other tests

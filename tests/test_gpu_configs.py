@@ -246,3 +246,76 @@ def test_sha512_many_mixed_lengths_unaligned(engine):
     got = d_out.cpu().numpy()
     bad = [i for i, m in enumerate(msgs) if bytes(got[i]) != hashlib.sha512(m).digest()]
     assert not bad, [(i, lens[i]) for i in bad[:10]]
+
+
+# ----------------------------------------------------------------------------- C4 headers
+def test_c4_headers_with_6667_parents():
+    """(f)2 at the size that motivates it: at N = 10,000 a header carries 2f+1 = 6,667 parents, so
+    Header::verify rehashes a 213,392-B preimage (primary/src/messages.rs:50, preimage :71-83) before
+    the certificate's 6,667-vote batch.  Through verify_certificates (Python orchestration) and the
+    native frame path (nw_certificates_verify): header digests vs hashlib, batch verdicts vs the C
+    oracle, and the reference's error order (InvalidHeaderId before the signatures)."""
+    import time
+    import hashlib as hl
+    from narwhal_amd import primary as pm
+    from narwhal_amd import workload
+    eng = _engine()
+    try:
+        wc = workload.make_committee(10000, eng)
+        keys = [bytes(k) for k in wc.pks]
+        seed_of = {bytes(k): bytes(s) for k, s in zip(wc.pks, wc.seeds)}
+        com = pm.Committee({k: (1, [0]) for k in keys})
+        assert com.quorum_threshold() == 6667
+        order = com.keys()
+        rng = np.random.default_rng(21)
+        certs = []
+        for r in range(4):
+            author = order[r * 13]
+            parents = [rng.bytes(32) for _ in range(6667)]
+            h = pm.Header(author, r + 1, {}, parents)
+            pre = h.digest_preimage()
+            assert len(pre) == 32 + 8 + 6667 * 32
+            h.id = hl.sha512(pre).digest()[:32]
+            _, hs = eng.sign_many_np(np.frombuffer(seed_of[author], np.uint8).reshape(1, 32),
+                                     np.frombuffer(h.id, np.uint8).reshape(1, 32))
+            h.signature = bytes(hs[0])
+            voters = [order[(r * 101 + k) % 10000] for k in range(6667)]
+            d = hl.sha512(pm.Vote(h.id, h.round, h.author, keys[0]).digest_preimage()).digest()[:32]
+            _, vs = eng.sign_many_np(np.stack([np.frombuffer(seed_of[v], np.uint8) for v in voters]),
+                                     np.tile(np.frombuffer(d, np.uint8), (6667, 1)))
+            certs.append(pm.Certificate(h, [(v, bytes(s)) for v, s in zip(voters, vs)]))
+        # cert 1: one parent byte changed after signing -> InvalidHeaderId; cert 2: one bad vote
+        p0 = sorted(certs[1].header.parents)[3000]
+        certs[1].header.parents.discard(p0)
+        certs[1].header.parents.add(bytes([p0[0] ^ 1]) + p0[1:])
+        k, s = certs[2].votes[4321]
+        certs[2].votes[4321] = (k, s[:40] + bytes([s[40] ^ 2]) + s[41:])
+        # GPU digests of the 213 KB preimages == hashlib
+        pres = [c.header.digest_preimage() for c in certs]
+        assert eng.sha512_many(pres) == [hl.sha512(p).digest() for p in pres]
+        zseed = bytes([3]) * 32
+        t0 = time.perf_counter()
+        got = pm.verify_certificates(certs, com, eng, zseed=zseed, cert_base=40)
+        t_py = time.perf_counter() - t0
+        frames = [pm.encode_primary_message(c) for c in certs]
+        t0 = time.perf_counter()
+        native = pm.verify_certificate_frames(frames, com, eng, zseed=zseed, cert_base=40)
+        t_nat = time.perf_counter() - t0
+        want_types = [None, pm.InvalidHeaderId, pm.InvalidSignature, None]
+        assert [type(e) if e else None for e in got] == want_types
+        assert [type(e) if e else None for e in native] == want_types
+        # the batch step vs the C oracle for the certificates that reach it (batch index = order
+        # among the certificates that reach the batch step, as nw_cert_batch_verify numbers them)
+        reach = [0, 2, 3]
+        for j, ci in enumerate(reach):
+            c = certs[ci]
+            dg = hl.sha512(c.digest_preimage()).digest()[:32]
+            want = nw_ref.crypto_verify_batch(dg, c.votes, zseed, 40 + j)
+            assert want == (ci != 2), ci
+        # one certificate alone through the native path: the Core::run latency at N = 10,000
+        one = pm.verify_certificate_frames(frames[:1], com, eng, zseed=zseed)
+        assert one == [None]
+        print("\n6,667-parent headers: 4 certs verify_certificates %.1f ms, native %.1f ms" % (t_py * 1e3,
+                                                                                         t_nat * 1e3))
+    finally:
+        eng.close()

@@ -179,6 +179,29 @@ def test_split_batch_partials(bare):
     assert split(hb) is False
 
 
+def test_empty_shards_and_batches(bare):
+    """Empty work on the MSM path: a zero-vote shard of a split batch (split_bounds gives
+    one whenever the batch has fewer votes than ranks) contributes the identity with no launch
+    error, and all-zero or partly-zero counts give dalek's empty-batch verdict, Ok."""
+    rng = random.Random(9)
+    zseed = bytes(rng.randrange(256) for _ in range(32))
+    pt, bad = bare.verify_batch_partial([], [], [], zseed, 3, 0)
+    assert not bad and bare.points_sum_is_identity([pt])
+    assert bare.verify_batches_pk([0], [], [], [], zseed) == [True]
+    assert bare.verify_batches_pk([0, 0, 0], [], [], [], zseed) == [True, True, True]
+    n = 5
+    seeds = [bytes(rng.randrange(256) for _ in range(32)) for _ in range(n)]
+    msg = bytes(rng.randrange(256) for _ in range(32))
+    pks, sigs = bare.sign_many(seeds, [msg] * n)
+    assert bare.verify_batches_pk([0, n, 0], [msg] * n, pks, sigs, zseed) == [True, True, True]
+    pts = []
+    for a, b in [(0, 0), (0, n), (n, n)]:   # two empty shards around the whole batch
+        p, bd = bare.verify_batch_partial([msg] * (b - a), pks[a:b], sigs[a:b], zseed, 4, a)
+        assert not bd
+        pts.append(p)
+    assert bare.points_sum_is_identity(pts)
+
+
 def test_uncached_then_cached_same_verdicts(golden):
     """A key that is verified before and after it enters the cache gets the same verdicts."""
     from narwhal_amd import _lib
