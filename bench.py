@@ -720,7 +720,8 @@ def main(argv=None):
         if world == 1 and c2 and not args.no_extras:
             out["host_fed"] = host_fed(eng, cs, slots, zseed)
             out["msm"] = msm_leg(eng)
-            out["latency"] = latency_legs(eng, com, slots, cs, args.latency_samples)
+            if args.latency_samples > 0:
+                out["latency"] = latency_legs(eng, com, slots, cs, args.latency_samples)
         if world == 1 and c2 and args.digest_batches > 0:
             out["digest"] = digest_leg(eng, dev, args.digest_batches, args.digest_share, 3,
                                        0.0 if args.no_cpu_baseline else 3.0, verify_step)

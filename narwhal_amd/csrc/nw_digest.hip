@@ -1,0 +1,214 @@
+// Bulk SHA-512 digests (worker batches, header / vote / certificate digests): sha2 0.9 Sha512 via
+// ed25519_dalek::Sha512 (primary/src/messages.rs:72-82,147-151,228-232; worker/src/processor.rs:65).
+//
+// A message is one Merkle-Damgard chain: block b+1 needs block b's state, so one message never uses
+// more than one instruction stream's worth of VALU per round.  What a lone wave sustains is one
+// instruction per ~4 cycles (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost'), so the latency
+// of a long message is its instruction count per block times that.  Two kernels:
+//
+//  * k_sha512_many  - one lane per message, everything in one wave: the throughput form (enough
+//                     messages to give every SIMD several waves).
+//  * k_sha512_split - few messages (worker batches: 1,250 per GPU at C4, a 6,667-parent header):
+//                     the message schedule does not depend on the chaining state, so a second wave
+//                     of the same workgroup computes K_t + W_t of block b+1 into LDS while the first
+//                     runs the 80 rounds of block b from LDS.  The round wave issues 27 VALU
+//                     instructions per round (Sigma1 8, Ch 2, Sigma0 8, Maj 2, 7 adds) + one LDS read,
+//                     instead of ~43 with the schedule inline; the two waves meet at one barrier per
+//                     block.
+#include <hip/hip_runtime.h>
+#include <cstdlib>
+#include "nw_sha512.h"
+#include "nw_kernels.h"
+
+namespace nw {
+
+// Blocks of the padded message of L bytes (L + 0x80 + 16-byte length, rounded up to 128).
+__device__ __forceinline__ uint32_t sha512_nblocks(uint64_t L) { return (uint32_t)((L + 17 + 127) / 128); }
+
+// Block b of the padded message (m, L) as 16 big-endian words.  Fast path: a full block at a
+// 4-byte-aligned address (32 dword loads).  Otherwise (the 1-2 padding blocks, or an unaligned
+// message): the aligned dwords that hold at least one message byte of the block are loaded (an
+// aligned dword holding a valid byte never leaves the message's page, so nothing past the buffer is
+// touched), realigned with v_alignbyte, and bytes past the message are masked to the padding.
+__device__ __forceinline__ void sha512_load_block(const uint8_t* m, uint64_t L, uint64_t b, uint64_t w[16]) {
+    const uint64_t nfull = L / 128;
+    const uintptr_t a0 = reinterpret_cast<uintptr_t>(m) + b * 128;
+    const uint32_t sh = (uint32_t)(a0 & 3u);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a0 - sh);
+    if (b < nfull && sh == 0) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) w[k] = be64_from_le32(q[2 * k], q[2 * k + 1]);
+        return;
+    }
+    const int64_t vrem = (int64_t)L - (int64_t)(b * 128);        // message bytes from this block on
+    const int32_t v = vrem <= 0 ? 0 : (vrem >= 128 ? 128 : (int32_t)vrem);
+    const bool marker = vrem >= 0 && vrem < 128;                // the 0x80 byte lands in this block
+    uint32_t u[33];
+    if (v + (int32_t)sh > 0) {
+        const int32_t kmax = (v + (int32_t)sh - 1) >> 2;          // last dword with a valid byte
+#pragma unroll
+        for (int k = 0; k < 33; ++k) u[k] = q[k < kmax ? k : kmax];
+    } else {
+#pragma unroll
+        for (int k = 0; k < 33; ++k) u[k] = 0u;
+    }
+    uint32_t x[32];
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+        const uint32_t t = __builtin_amdgcn_alignbyte(u[j + 1], u[j], sh);   // block bytes 4j .. 4j+3
+        const int32_t d = v - 4 * j;                                         // valid bytes in this word
+        uint32_t r = d >= 4 ? t : (d <= 0 ? 0u : (t & ((1u << (8 * d)) - 1u)));
+        if (marker && d >= 0 && d < 4) r |= 0x80u << (8 * d);
+        x[j] = r;
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = be64_from_le32(x[2 * k], x[2 * k + 1]);
+    if (b + 1 == sha512_nblocks(L)) {
+        w[14] = L >> 61;
+        w[15] = L << 3;
+    }
+}
+
+NW_HD void sha512_digest_store(uint8_t* out, const uint64_t st[8]) {
+    uint32_t d[16];
+    sha512_digest_le32(d, st);
+    uint4* o = reinterpret_cast<uint4*>(out);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
+}
+
+// ------------------------------------------------------------------------------------ one lane per message
+// Throughput form: bounded to 128 VGPRs so 4 waves share each SIMD (a lone wave issues one VALU
+// instruction per ~4 cycles; several waves per SIMD approach the SIMD's full rate).
+__global__ void __launch_bounds__(256, 4) k_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off,
+                                                        const uint64_t* len, uint8_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* m = base + off[i];
+    const uint64_t L = len[i];
+    uint64_t st[8];
+    sha512_init(st);
+    const uint32_t nb = sha512_nblocks(L);
+    for (uint32_t b = 0; b < nb; ++b) {
+        uint64_t w[16];
+        sha512_load_block(m, L, b, w);
+        sha512_compress(st, w);
+    }
+    sha512_digest_store(out + (size_t)i * 64, st);
+}
+
+// ------------------------------------------------------------------------------------ schedule / round split
+static constexpr uint32_t SPLIT_MSGS = 64;        // messages per workgroup: lane L of both waves
+static constexpr uint32_t SPLIT_MAX_N = 32768;    // above: k_sha512_many (every SIMD has work anyway)
+
+// t1 = h + (K_t + W_t) + Sigma1(e) + Ch(e, f, g); t2 = Sigma0(a) + Maj(a, b, c)
+#define NW_SHA_ROUND_KW(a, b, c, d, e, f, g, h, kw)                                                     \
+    do {                                                                                                \
+        const uint64_t t1 = (h) + (kw) + xor3_64(rotr64((e), 14), rotr64((e), 18), rotr64((e), 41)) +     \
+                            ch64((e), (f), (g));                                                        \
+        const uint64_t t2 = xor3_64(rotr64((a), 28), rotr64((a), 34), rotr64((a), 39)) + maj64((a), (b), (c)); \
+        (d) += t1;                                                                                      \
+        (h) = t1 + t2;                                                                                  \
+    } while (0)
+
+// Schedule wave: K_t + W_t for t = 0..79 of block b into kwb[t][lane].
+__device__ __forceinline__ void split_schedule(const uint8_t* m, uint64_t L, uint64_t b, uint64_t (*kwb)[SPLIT_MSGS],
+                                               uint32_t lane) {
+    uint64_t w[16];
+    sha512_load_block(m, L, b, w);
+#pragma unroll
+    for (int t = 0; t < 16; ++t) kwb[t][lane] = w[t] + SHA512_K[t];
+#pragma unroll
+    for (int r = 16; r < 80; r += 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+            const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
+            const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
+            w[i] += s0 + w[(i + 9) & 15] + s1;
+            kwb[r + i][lane] = w[i] + SHA512_K[r + i];
+        }
+    }
+}
+
+// Round wave: the 80 rounds of one block with K_t + W_t from LDS (16 words loaded one group ahead).
+__device__ __forceinline__ void split_rounds(uint64_t st[8], const uint64_t (*kwb)[SPLIT_MSGS], uint32_t lane) {
+    uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+    uint64_t k0[16], k1[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) k0[q] = kwb[q][lane];
+#pragma unroll
+    for (int grp = 0; grp < 5; ++grp) {
+        if (grp < 4) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) k1[q] = kwb[(grp + 1) * 16 + q][lane];
+        }
+        NW_SHA_ROUND_KW(a, b, c, d, e, f, g, h, k0[0]);
+        NW_SHA_ROUND_KW(h, a, b, c, d, e, f, g, k0[1]);
+        NW_SHA_ROUND_KW(g, h, a, b, c, d, e, f, k0[2]);
+        NW_SHA_ROUND_KW(f, g, h, a, b, c, d, e, k0[3]);
+        NW_SHA_ROUND_KW(e, f, g, h, a, b, c, d, k0[4]);
+        NW_SHA_ROUND_KW(d, e, f, g, h, a, b, c, k0[5]);
+        NW_SHA_ROUND_KW(c, d, e, f, g, h, a, b, k0[6]);
+        NW_SHA_ROUND_KW(b, c, d, e, f, g, h, a, k0[7]);
+        NW_SHA_ROUND_KW(a, b, c, d, e, f, g, h, k0[8]);
+        NW_SHA_ROUND_KW(h, a, b, c, d, e, f, g, k0[9]);
+        NW_SHA_ROUND_KW(g, h, a, b, c, d, e, f, k0[10]);
+        NW_SHA_ROUND_KW(f, g, h, a, b, c, d, e, k0[11]);
+        NW_SHA_ROUND_KW(e, f, g, h, a, b, c, d, k0[12]);
+        NW_SHA_ROUND_KW(d, e, f, g, h, a, b, c, k0[13]);
+        NW_SHA_ROUND_KW(c, d, e, f, g, h, a, b, k0[14]);
+        NW_SHA_ROUND_KW(b, c, d, e, f, g, h, a, k0[15]);
+        if (grp < 4) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) k0[q] = k1[q];
+        }
+    }
+    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
+    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+}
+
+// 128 threads: wave 0 = rounds, wave 1 = schedule; lane L of both waves serves message
+// 64 * blockIdx.x + L.  kw is double-buffered: while wave 0 compresses block b from kw[b & 1],
+// wave 1 fills kw[(b + 1) & 1]; one barrier per block.  Both waves derive the same trip count (the
+// largest block count of the workgroup's messages), so every barrier is reached by both.
+__global__ void __launch_bounds__(128) k_sha512_split(uint32_t n, const uint8_t* base, const uint64_t* off,
+                                                      const uint64_t* len, uint8_t* out) {
+    __shared__ uint64_t kw[2][80][SPLIT_MSGS];    // 81,920 B: two workgroups per CU
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool sched = threadIdx.x >= 64;         // wave-uniform
+    const uint32_t i = blockIdx.x * SPLIT_MSGS + lane;
+    const bool live = i < n;
+    const uint64_t L = live ? len[i] : 0;
+    const uint8_t* m = base + (live ? off[i] : 0);
+    const uint32_t nb = live ? sha512_nblocks(L) : 0u;
+    uint32_t nbmax = nb;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, o, 64));
+    if (sched && nb > 0) split_schedule(m, L, 0, kw[0], lane);
+    __syncthreads();
+    uint64_t st[8];
+    sha512_init(st);
+    for (uint32_t b = 0; b < nbmax; ++b) {
+        if (sched) {
+            if (b + 1 < nb) split_schedule(m, L, b + 1, kw[(b + 1) & 1], lane);
+        } else if (b < nb) {
+            split_rounds(st, kw[b & 1], lane);
+        }
+        __syncthreads();
+    }
+    if (!sched && live) sha512_digest_store(out + (size_t)i * 64, st);
+}
+
+hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off, const uint64_t* len,
+                              uint8_t* out, hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    static const bool nosplit = std::getenv("NW_SHA_NOSPLIT") != nullptr;   // A/B knob (tools/)
+    if (n <= SPLIT_MAX_N && !nosplit)
+        hipLaunchKernelGGL(k_sha512_split, dim3(blocks_for(n, SPLIT_MSGS)), dim3(128), 0, st, n, base, off, len, out);
+    else
+        hipLaunchKernelGGL(k_sha512_many, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, base, off, len, out);
+    return hipGetLastError();
+}
+
+}  // namespace nw

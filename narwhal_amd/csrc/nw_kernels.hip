@@ -300,79 +300,6 @@ __global__ void __launch_bounds__(256) k_flags_to_ok(uint32_t n, const uint32_t*
     if (i < n) ok[i] = (flags[i] & NW_F_STRICT) ? 1 : 0;
 }
 
-// ------------------------------------------------------------------------------------ SHA-512 bulk
-// One lane per message (each message is an inherently sequential compression chain).
-__global__ void __launch_bounds__(256) k_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off,
-                                                     const uint64_t* len, uint8_t* out) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint8_t* m = base + off[i];
-    const uint64_t L = len[i];
-    const uint64_t nfull = L / 128;
-    uint64_t st[8];
-    sha512_init(st);
-    uint64_t w[16];
-    const bool aligned = (reinterpret_cast<uintptr_t>(m) & 3u) == 0;
-    if (aligned && nfull) {
-        // One wave per SIMD at worker-batch counts: nothing else hides the load latency, so the
-        // next block's 32 words are loaded before the current block is compressed.
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(m);
-        uint32_t nx[32];
-#pragma unroll
-        for (int k = 0; k < 32; ++k) nx[k] = p[k];
-        for (uint64_t b = 0; b < nfull; ++b) {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) w[k] = be64_from_le32(nx[2 * k], nx[2 * k + 1]);
-            if (b + 1 < nfull) {
-                const uint32_t* q = p + (b + 1) * 32;
-#pragma unroll
-                for (int k = 0; k < 32; ++k) nx[k] = q[k];
-            }
-            sha512_compress(st, w);
-        }
-    }
-    for (uint64_t b = 0; !aligned && b < nfull; ++b) {
-        const uint8_t* blk = m + b * 128;
-        {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                uint64_t x = 0;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) x = (x << 8) | blk[8 * k + j];
-                w[k] = x;
-            }
-        }
-        sha512_compress(st, w);
-    }
-    // tail: remaining bytes + padding (1 or 2 blocks)
-    const uint64_t rem = L - nfull * 128;
-    const uint8_t* tail = m + nfull * 128;
-    const int tb = rem + 17 <= 128 ? 1 : 2;
-    for (int b = 0; b < tb; ++b) {
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            uint64_t x = 0;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint64_t p = (uint64_t)b * 128 + 8 * k + j;
-                const uint32_t byte = p < rem ? tail[p] : (p == rem ? 0x80u : 0u);
-                x = (x << 8) | byte;
-            }
-            w[k] = x;
-        }
-        if (b == tb - 1) {
-            w[14] = L >> 61;
-            w[15] = L << 3;
-        }
-        sha512_compress(st, w);
-    }
-    uint32_t d[16];
-    sha512_digest_le32(d, st);
-    uint4* o = reinterpret_cast<uint4*>(out + (size_t)i * 64);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) o[k] = make_uint4(d[4 * k], d[4 * k + 1], d[4 * k + 2], d[4 * k + 3]);
-}
-
 // ------------------------------------------------------------------------------------ launchers
 static hipError_t launch_vs(const VerifyParams& p, int msgmode, int key_window, bool slow, uint32_t n_upper,
                             hipStream_t st) {
@@ -449,13 +376,6 @@ hipError_t launch_validate_certs(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys
 hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hipStream_t st) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_flags_to_ok, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, flags, ok);
-    return hipGetLastError();
-}
-
-hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off, const uint64_t* len,
-                              uint8_t* out, hipStream_t st) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_sha512_many, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, base, off, len, out);
     return hipGetLastError();
 }
 

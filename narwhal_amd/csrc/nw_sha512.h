@@ -69,7 +69,9 @@ NW_HD uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
         : "=v"(lo) : "v"((uint32_t)a), "v"((uint32_t)b), "v"((uint32_t)c), "i"(TT));
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:%4"
         : "=v"(hi) : "v"((uint32_t)(a >> 32)), "v"((uint32_t)(b >> 32)), "v"((uint32_t)(c >> 32)), "i"(TT));
-    return ((uint64_t)hi << 32) | lo;
+    uint64_t r = ((uint64_t)hi << 32) | lo;
+    asm("" : "+v"(r));   // opaque: keeps LLVM from splitting later 64-bit adds over the halves
+    return r;
 #else
     uint64_t r = 0;
     for (int bit = 0; bit < 64; ++bit) {
@@ -85,6 +87,10 @@ NW_HD uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0x
 // Maj(a, b, c) = (a & b) | (a & c) | (b & c)
 NW_HD uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0xE8>(a, b, c); }
 
+// Ch(e, f, g) = (e & f) ^ (~e & g) as one bitop3 per half (LLVM otherwise splits it into an AND and
+// a BFI whose disjoint halves it then adds separately)
+NW_HD uint64_t ch64(uint64_t e, uint64_t f, uint64_t g) { return bitop3_64<0xCA>(e, f, g); }
+
 // big-endian 64-bit word from two little-endian-loaded u32 (bytes b0..b3 in lo, b4..b7 in hi)
 NW_HD uint64_t be64_from_le32(uint32_t lo, uint32_t hi) {
     return ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
@@ -93,7 +99,7 @@ NW_HD uint64_t be64_from_le32(uint32_t lo, uint32_t hi) {
 #define NW_SHA_ROUND(a, b, c, d, e, f, g, h, k, w)                                        \
     do {                                                                                    \
         const uint64_t t1 = (h) + xor3_64(rotr64((e), 14), rotr64((e), 18), rotr64((e), 41)) + \
-                            (((e) & (f)) ^ (~(e) & (g))) + (k) + (w);                       \
+                            ch64((e), (f), (g)) + (k) + (w);                       \
         const uint64_t t2 = xor3_64(rotr64((a), 28), rotr64((a), 34), rotr64((a), 39)) +   \
                             maj64((a), (b), (c));                                           \
         (d) += t1;                                                                          \

@@ -319,3 +319,32 @@ def test_c4_headers_with_6667_parents():
                                                                                          t_nat * 1e3))
     finally:
         eng.close()
+
+
+def test_sha512_throughput_kernel_many_messages(engine):
+    """More messages than the schedule/round split serves (> 32,768: k_sha512_many, one lane per
+    message, 4+ waves per SIMD): mixed lengths across the 111/112/128-byte padding boundaries at
+    unaligned offsets, vs hashlib."""
+    import torch
+    rng = np.random.default_rng(23)
+    n = 40000
+    lens = rng.integers(0, 700, size=n)
+    lens[:8] = [0, 111, 112, 127, 128, 129, 239, 256]
+    offs = np.zeros(n, np.int64)
+    pos = 1
+    for i in range(n):
+        offs[i] = pos
+        pos += int(lens[i]) + int(rng.integers(0, 4))
+    blob = rng.integers(0, 256, size=pos + 8, dtype=np.uint8)
+    dev = torch.device("cuda", 0)
+    d_blob = torch.from_numpy(blob).to(dev)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int64)).to(dev)
+    d_out = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
+    engine.sha512_many_dev(d_blob.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_out.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy()
+    bad = [i for i in range(n)
+           if bytes(got[i]) != hashlib.sha512(blob[offs[i]:offs[i] + lens[i]].tobytes()).digest()]
+    assert not bad, [(i, int(lens[i]), int(offs[i])) for i in bad[:10]]

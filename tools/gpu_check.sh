@@ -27,4 +27,9 @@ f=$(find $OUT/prof_all -name '*kernel_stats.csv' | head -1)
 f=$(find $OUT/prof_all -name '*kernel_trace.csv' | head -1)
 [ -n "$f" ] && grep -E "k_sha512_many|k_verify|Kernel_Name" "$f" | cut -c1-400 > $OUT/trace_sha_verify.csv
 fi
+if [ -n "$TRACE_ONECALL" ]; then
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $OUT/prof_onecall -o t -- python3 tools/one_call_trace.py > $OUT/onecall.log 2>&1 || { echo "ONECALL FAILED"; tail -20 $OUT/onecall.log; exit 1; }
+grep '^{' $OUT/onecall.log
+python3 tools/one_call_trace.py --analyze $OUT/prof_onecall > $OUT/onecall_anatomy.txt 2>&1; tail -12 $OUT/onecall_anatomy.txt | cut -c1-600
+fi
 exit 0
