@@ -99,7 +99,7 @@ struct Workspace {
     DevBuf w_sig, w_signer, w_keys, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len, w_flags,
         w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_ok, w_misc, w_out, w_pbuf, w_pre, w_counts,
         w_cursor, w_perm, w_io, w_var, w_status, w_msm_ent, w_msm_dig, w_msm_zs, w_msm_meta, w_msm_bkt, w_msm_part,
-        w_msm_wpart;
+        w_msm_wpart, w_pslow, w_cert_state;
     HostBuf h_io, h_meta;
 
     // Grow a buffer; a buffer that may still be read by a pending call is only freed after it.
@@ -116,7 +116,7 @@ struct Workspace {
                           &w_msg_len, &w_flags, &w_slow_count, &w_slow_list, &w_slow_slot, &w_slow_buf, &w_cert_ok,
                           &w_ok, &w_misc, &w_out, &w_pbuf, &w_pre, &w_counts, &w_cursor, &w_perm, &w_io, &w_var,
                           &w_status, &w_msm_ent, &w_msm_dig, &w_msm_zs, &w_msm_meta, &w_msm_bkt, &w_msm_part,
-                          &w_msm_wpart})
+                          &w_msm_wpart, &w_pslow, &w_cert_state})
             b->release();
         h_io.release();
         h_meta.release();
@@ -454,7 +454,11 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     NW_TRY(ws->ensure(ws->w_slow_count, 16), "ws slow_count");
     NW_TRY(ws->ensure(ws->w_slow_list, nsigs * 4 + 4), "ws slow_list");
     NW_TRY(ws->ensure(ws->w_slow_slot, nsigs * 4 + 4), "ws slow_slot");
-    if (batch_mode) NW_TRY(ws->ensure(ws->w_slow_buf, nsigs * (size_t)SLOW_WORDS * 4 + 4), "ws slow_buf");
+    if (batch_mode) {
+        NW_TRY(ws->ensure(ws->w_slow_buf, nsigs * (size_t)SLOW_WORDS * 4 + 4), "ws slow_buf");
+        NW_TRY(ws->ensure(ws->w_pslow, nsigs * (size_t)160 + 16), "ws pslow");
+        NW_TRY(ws->ensure(ws->w_cert_state, ncerts * 4 + 16), "ws cert_state");
+    }
     NW_TRY(ws->ensure(ws->w_pbuf, nsigs * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
     NW_TRY(ws->ensure(ws->w_pre, nsigs * 40 + 16), "ws pre");
     // signer grouping (device counting sort) when keys repeat
@@ -470,7 +474,8 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     // signer slots; check the device inputs into d_status (when given).
     NW_TRY(launch_prep_expand((uint32_t)ncerts, (uint32_t)nsigs, (uint32_t)ctx->nkeys, d_first, d_nv, d_signer,
                               ws->w_sig_cert.as<uint32_t>(), ws->w_slow_count.as<uint32_t>(),
-                              group ? ws->w_counts.as<uint32_t>() : nullptr, d_status, st),
+                              group ? ws->w_counts.as<uint32_t>() : nullptr, d_status,
+                              batch_mode ? ws->w_cert_state.as<uint32_t>() : nullptr, st),
            "k_prep_certs / k_expand_count");
 
     VerifyParams vp{};
@@ -497,6 +502,8 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     vp.slow_list = ws->w_slow_list.as<uint32_t>();
     vp.slow_slot = ws->w_slow_slot.as<uint32_t>();
     vp.slow_buf = ws->w_slow_buf.as<uint32_t>();
+    vp.pslow = batch_mode ? ws->w_pslow.as<uint32_t>() : nullptr;
+    vp.cert_state = batch_mode ? ws->w_cert_state.as<uint32_t>() : nullptr;
     vp.pbuf = ws->w_pbuf.as<uint32_t>();
     vp.pre = ws->w_pre.as<uint32_t>();
     vp.perm = nullptr;
@@ -533,7 +540,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
         return NW_OK;
     }
 
-    NW_TRY(launch_slow(vp, msgmode, ctx->key_window, (uint32_t)nsigs, st), "k_slow_sig");
+    NW_TRY(launch_slow(vp, msgmode, ctx->key_window, (uint32_t)nsigs, st), "k_slow_prep / k_slow_mul");
 
     FinalizeParams fp{};
     fp.ncerts = (uint32_t)ncerts;
@@ -545,6 +552,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     fp.stake = ctx->d_stake;
     fp.slow_slot = vp.slow_slot;
     fp.slow_buf = vp.slow_buf;
+    fp.cert_state = vp.cert_state;
     fp.cert_ok = d_cert_ok;
     fp.accepted_stake = d_stake_out;
     fp.sig_ok = d_sig_ok;

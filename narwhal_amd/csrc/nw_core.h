@@ -8,6 +8,12 @@
 
 namespace nw {
 
+// Batch coefficient z_i of vote i of certificate ``cert`` (NW-Z v1: nonce = global certificate index).
+__device__ __forceinline__ void coeff_z(const VerifyParams& a, uint32_t i, uint32_t cert, uint32_t z4[4]) {
+    const uint64_t bidx = a.cert_base + cert;
+    chacha20_z(z4, a.zseed, i - a.cert_first[cert], (uint32_t)bidx, (uint32_t)(bidx >> 32), 0u);
+}
+
 // ------------------------------------------------------------------------------------ loads
 NW_HD void load_w8(uint32_t w[8], const uint32_t* p) {
     const uint4 a = reinterpret_cast<const uint4*>(p)[0];

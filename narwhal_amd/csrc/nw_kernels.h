@@ -11,7 +11,22 @@ static constexpr uint32_t KI_OK = 1u;             // decodes (dalek::PublicKey::
 static constexpr uint32_t KI_SMALL = 2u;          // small order
 static constexpr uint32_t KI_TORSION_SHIFT = 4;   // 3 bits: t with A^t = t * T8
 static constexpr uint32_t NW_F_TCOEF_SHIFT = 8;   // 3 bits of per-signature torsion coefficient
-static constexpr int SLOW_WORDS = 40;             // slow-path record: extended point z_i (R_i - P_i)
+// Exact-path record of a signature whose strict equation fails (k_slow_prep / k_slow_mul /
+// k_cert_finalize): an extended point (D_i = R_i - P_i, or z_i D_i once multiplied), its kind, and
+// z_i mod 8.
+static constexpr int SLOW_WORDS = 44;
+static constexpr int SLOW_KIND = 40;              // word: SK_*
+static constexpr int SLOW_Z8 = 41;                // word: z_i mod 8 (SK_SMALL)
+static constexpr uint32_t SK_SKIP = 0;            // certificate already rejected: no point computed
+static constexpr uint32_t SK_SMALL = 1;           // D_i of small order (or z_i = 0): z_i D_i = (z_i mod 8) D_i
+static constexpr uint32_t SK_BIG = 2;             // D_i has a prime-order component and z_i != 0
+static constexpr uint32_t SK_MUL = 3;             // SK_BIG whose z_i D_i was computed (record holds z_i D_i)
+// Per-certificate exact-path state word: the number of SK_BIG entries, and a flag set as soon as
+// the certificate is known to be rejected (a vote with bad S / undecodable A / undecodable R).
+static constexpr uint32_t CS_DOOM = 0x80000000u;
+static constexpr uint32_t CS_BIG_MASK = 0x7FFFFFFFu;
+// internal flag bit: k_verify parked P_i (extended) in pslow[i] (its y did not match R's)
+static constexpr uint32_t NW_F_P_SAVED = 0x4000u;
 static constexpr int PBUF_WORDS = 21;             // per-signature k_verify -> k_finish record (X, Z, flags)
 #ifndef NW_FINISH_K
 #define NW_FINISH_K 16
@@ -44,6 +59,8 @@ struct VerifyParams {
     uint32_t* slow_list;           // [n]
     uint32_t* slow_slot;           // [n]
     uint32_t* slow_buf;            // [n][SLOW_WORDS]
+    uint32_t* pslow;               // [n][40] P_i of signatures whose y did not match (batch mode; may be null)
+    uint32_t* cert_state;          // [ncerts] CS_* exact-path state (batch mode)
     uint32_t* pbuf;                // [PREC_ROWS][n] SoA, processing order: P's X, Z + partial flags
     uint32_t* pre;                 // [10][n] SoA prefix products of Z (k_finish scratch)
     const uint32_t* perm;          // [n] processing order for k_verify (signer-grouped) or null
@@ -61,6 +78,7 @@ struct FinalizeParams {
     const uint32_t* stake;         // [K]
     const uint32_t* slow_slot;
     const uint32_t* slow_buf;
+    const uint32_t* cert_state;    // [ncerts] CS_*
     uint8_t* cert_ok;              // [ncerts] (may be null)
     uint64_t* accepted_stake;      // [ncerts] (may be null)
     uint8_t* sig_ok;               // [nsigs] strict verdict bytes (may be null; k_flags_to_ok fused)
@@ -68,6 +86,9 @@ struct FinalizeParams {
 
 hipError_t launch_verify(const VerifyParams& p, int msgmode, int key_window, hipStream_t st);
 hipError_t launch_finish(const VerifyParams& p, hipStream_t st);
+// Exact path of the batch equation: k_slow_prep (every signature with D_i != O: decode R, D_i,
+// small-order test) then k_slow_mul (z_i D_i, only for certificates with two or more SK_BIG
+// entries); both read the device slow counter, so honest batches find no work.
 hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st);
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st);
 // Batch preamble: zero sig_cert / counts (may be null: no histogram) / the slow counter / status (may
@@ -75,7 +96,7 @@ hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st);
 // k_expand_count); then launch_group_scatter (scan + scatter) when counts were built.
 hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
                               const uint32_t* nv, const uint32_t* signer, uint32_t* sig_cert, uint32_t* zero4,
-                              uint32_t* counts, uint32_t* status, hipStream_t st);
+                              uint32_t* counts, uint32_t* status, uint32_t* cert_state, hipStream_t st);
 hipError_t launch_group_scatter(uint32_t n, uint32_t nkeys, const uint32_t* signer, const uint32_t* counts,
                                 uint32_t* cursor, uint32_t* perm, hipStream_t st);
 hipError_t launch_validate_certs(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,

@@ -9,19 +9,20 @@
 // decomposes exactly (with D_i = R_i - P_i, A_i^t the 8-torsion part of A_i, l = 5 mod 8) into
 //     sum_i z_i D_i  +  sum_i ((r_i - z_i h_i) mod 8) A_i^t == O,      r_i = z_i h_i mod l,
 // so a certificate whose signatures all satisfy D_i = O and whose keys are torsion-free is accepted
-// without any variable-base work; everything else goes to the exact path (k_slow_sig), which
-// evaluates the remaining terms literally.  Verdicts are therefore identical to dalek's for every
+// without any variable-base work; everything else goes to the exact path (k_slow_prep, k_slow_mul),
+// which decides the remaining terms exactly.  Verdicts are therefore identical to dalek's for every
 // input (not just honest ones) given the same z_i.
 //
 // Pipeline per batch: k_prep_certs + k_expand_count -> [signer grouping] -> k_verify (P_i, one lane per signature)
 // -> k_finish (Montgomery batch inversion of Z over FINISH_K signatures per lane, encoding match,
-// strict verdict) -> k_slow_sig (compacted list of mismatches only) -> k_cert_finalize.
+// strict verdict) -> k_slow_prep / k_slow_mul (compacted list of mismatches only) -> k_cert_finalize.
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include "nw_point.h"
 #include "nw_sha512.h"
 #include "nw_kernels.h"
 #include "nw_core.h"
+#include "nw_quad.h"
 
 namespace nw {
 
@@ -147,11 +148,17 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
             }
             const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
             uint32_t f = finish_x_flags(load_fe_soa(a.pbuf, n, g), zi, a.pbuf[PREC_FLAGS_ROW * n + g]);
-            if (a.batch_mode && (f & (NW_F_S_OK | NW_F_A_OK)) == (NW_F_S_OK | NW_F_A_OK) && !(f & NW_F_MATCH)) {
-                f |= NW_F_SLOW;
-                const uint32_t t = atomicAdd(a.slow_count, 1u);
-                a.slow_list[t] = i;
-                a.slow_slot[i] = t;
+            if (a.batch_mode) {
+                if ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) {
+                    // the certificate is rejected (dalek: parse / decode error before the MSM): no
+                    // exact-path work for any of its votes
+                    atomicOr(&a.cert_state[a.sig_cert[i]], CS_DOOM);
+                } else if (!(f & NW_F_MATCH)) {
+                    f |= NW_F_SLOW;
+                    const uint32_t t = atomicAdd(a.slow_count, 1u);
+                    a.slow_list[t] = i;
+                    a.slow_slot[i] = t;
+                }
             }
             a.flags[i] = f;
         }
@@ -204,13 +211,29 @@ __global__ void __launch_bounds__(256, NW_FINALIZE_WAVES) k_cert_finalize(Finali
         ok = false;
     } else if (!slow) {
         ok = (tsum & 7u) == 0;
+    } else if ((a.cert_state[c] & CS_BIG_MASK) == 1u) {
+        ok = false;   // one term with a prime-order component: the sum cannot be the identity (k_slow_prep)
     } else {
-        // exact sum of the slow-path terms: lanes stride over the votes, then a shuffle tree
+        // exact sum of the slow-path terms: z_i D_i computed by k_slow_mul (SK_MUL), or (z_i mod 8) D_i
+        // for small-order D_i (SK_SMALL, at most 3 doublings + 3 additions); lanes stride over the
+        // votes, then a shuffle tree
         ge_p3 acc = ge_to_vgpr(ge_identity());
         for (uint32_t v = lane; v < nv; v += 64) {
             if (a.flags[first + v] & NW_F_SLOW) {
-                const ge_p3 Q = load_p3(a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS);
-                acc = ge_add(acc, ge_to_cached(Q));
+                const uint32_t* rec = a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS;
+                const ge_p3 Q = load_p3(rec);
+                if (rec[SLOW_KIND] == SK_MUL) {
+                    acc = ge_add(acc, ge_to_cached(Q));
+                } else {
+                    const uint32_t z8 = rec[SLOW_Z8];
+                    const ge_cached qc = ge_to_cached(Q);
+                    ge_p3 m = ge_to_vgpr(ge_identity());
+                    for (int bit = 2; bit >= 0; --bit) {
+                        m = ge_dbl(m);
+                        if ((z8 >> bit) & 1u) m = ge_add(m, qc);
+                    }
+                    acc = ge_add(acc, ge_to_cached(m));
+                }
             }
         }
 #pragma unroll
@@ -247,10 +270,13 @@ __global__ void __launch_bounds__(256) k_validate_certs(uint32_t ncerts, uint32_
 //                   signature tile b (GROUP_TILE signatures), histograms the signer slots (LDS, one
 //                   global add per slot) and/or checks them; every check ORs NW_ERR_ARG into status.
 __global__ void __launch_bounds__(256) k_prep_certs(uint32_t nsigs, uint32_t nkeys, uint32_t* sig_cert, uint32_t* counts,
-                                                    uint32_t* zero4, uint32_t* status) {
+                                                    uint32_t* zero4, uint32_t* status, uint32_t ncerts,
+                                                    uint32_t* cert_state) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t i = t; i <= nsigs; i += stride) sig_cert[i] = 0u;
+    if (cert_state)
+        for (uint32_t c = t; c < ncerts; c += stride) cert_state[c] = 0u;
     if (counts)
         for (uint32_t k = t; k < nkeys; k += stride) counts[k] = 0u;
     if (t < 4) zero4[t] = 0u;
@@ -300,6 +326,69 @@ __global__ void __launch_bounds__(256) k_flags_to_ok(uint32_t n, const uint32_t*
     if (i < n) ok[i] = (flags[i] & NW_F_STRICT) ? 1 : 0;
 }
 
+// ------------------------------------------------------------------------------------ exact path, step 2
+// z_i D_i for the SK_BIG entries of certificates that have two or more of them (the only case the
+// direct-sum argument of k_slow_prep cannot decide): one quad per entry, every point operation
+// split over the quad's 4 lanes (nw_quad.h), signed radix-16 digits of the 128-bit z_i with the
+// multiples 1..8 D_i in LDS: 7 table operations + 128 doublings + 32 additions on the quad.
+static constexpr uint32_t SLOW_MUL_QUADS = 16;   // per 64-thread workgroup
+__global__ void __launch_bounds__(64) k_slow_mul(VerifyParams a) {
+    __shared__ uint32_t tab[SLOW_MUL_QUADS][8][40];
+    const uint32_t cnt = *a.slow_count;
+    const uint32_t qd = threadIdx.x >> 2, q = threadIdx.x & 3u;
+    uint32_t (*T)[40] = tab[qd];
+    for (uint32_t t = blockIdx.x * SLOW_MUL_QUADS + qd; t < cnt; t += gridDim.x * SLOW_MUL_QUADS) {
+        uint32_t* rec = a.slow_buf + (size_t)t * SLOW_WORDS;
+        if (rec[SLOW_KIND] != SK_BIG) continue;                      // uniform over the quad
+        const uint32_t i = a.slow_list[t];
+        const uint32_t cert = a.sig_cert[i];
+        const uint32_t cs = a.cert_state[cert];
+        if ((cs & CS_DOOM) || (cs & CS_BIG_MASK) < 2u) continue;
+        const ge_p3 D = ge_to_vgpr(load_p3(rec));
+        uint32_t z4[4];
+        coeff_z(a, i, cert, z4);
+        // T[k] = (k + 1) D
+        ge_p3 m = D;
+        if (q == 0) store_p3(T[0], m);
+        m = ge_dbl_quad(D);
+        if (q == 0) store_p3(T[1], m);
+#pragma nounroll
+        for (int k = 2; k < 8; ++k) {
+            m = ge_add_quad(m, D);
+            if (q == 0) store_p3(T[k], m);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // signed radix-16 digits d_0..d_31 in [-8, 8) plus a top carry d_32 in {0, 1}, packed as
+        // nibbles with d_31 in the top nibble so the Horner loop shifts them out from the top
+        uint32_t pk[4] = {0u, 0u, 0u, 0u};
+        uint32_t carry = 0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const uint32_t b = ((z4[j >> 3] >> (4 * (j & 7))) & 15u) + carry;
+            carry = b >= 8u ? 1u : 0u;
+            pk[j >> 3] |= ((b - 16u * carry) & 15u) << (4 * (j & 7));
+        }
+        ge_p3 acc = ge_select(ge_to_vgpr(ge_identity()), D, carry != 0);
+#pragma nounroll
+        for (int j = 31; j >= 0; --j) {
+            acc = ge_dbl_quad(ge_dbl_quad(ge_dbl_quad(ge_dbl_quad(acc))));
+            const int d = (int)(pk[3] << 0) >> 28;                  // top nibble, sign-extended
+#pragma unroll
+            for (int w = 3; w > 0; --w) pk[w] = (pk[w] << 4) | (pk[w - 1] >> 28);
+            pk[0] <<= 4;
+            if (d != 0) {
+                const ge_p3 e = load_p3(T[(d < 0 ? -d : d) - 1]);
+                acc = ge_add_quad(acc, d < 0 ? ge_neg(e) : e);
+            }
+        }
+        if (q == 0) {
+            store_p3(rec, acc);
+            rec[SLOW_KIND] = SK_MUL;
+        }
+        __builtin_amdgcn_wave_barrier();   // the table slot is rewritten by this quad's next entry
+    }
+}
+
 // ------------------------------------------------------------------------------------ launchers
 static hipError_t launch_vs(const VerifyParams& p, int msgmode, int key_window, bool slow, uint32_t n_upper,
                             hipStream_t st) {
@@ -319,7 +408,11 @@ hipError_t launch_verify(const VerifyParams& p, int msgmode, int key_window, hip
 
 hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st) {
     if (n_upper == 0) return hipSuccess;
-    return launch_vs(p, msgmode, key_window, true, n_upper, st);
+    hipError_t e = launch_vs(p, msgmode, key_window, true, n_upper, st);
+    if (e != hipSuccess) return e;
+    const uint32_t nb = std::min<uint32_t>(blocks_for(n_upper, SLOW_MUL_QUADS), 256u);
+    hipLaunchKernelGGL(k_slow_mul, dim3(nb), dim3(64), 0, st, p);
+    return hipGetLastError();
 }
 
 hipError_t launch_finish(const VerifyParams& p, hipStream_t st) {
@@ -338,9 +431,10 @@ hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
 
 hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
                               const uint32_t* nv, const uint32_t* signer, uint32_t* sig_cert, uint32_t* zero4,
-                              uint32_t* counts, uint32_t* status, hipStream_t st) {
-    const uint32_t prep_blocks = std::min<uint32_t>(blocks_for(nsigs + 1, 256), 1024u);
-    hipLaunchKernelGGL(k_prep_certs, dim3(prep_blocks), dim3(256), 0, st, nsigs, nkeys, sig_cert, counts, zero4, status);
+                              uint32_t* counts, uint32_t* status, uint32_t* cert_state, hipStream_t st) {
+    const uint32_t prep_blocks = std::min<uint32_t>(blocks_for(std::max(nsigs + 1, ncerts), 256), 1024u);
+    hipLaunchKernelGGL(k_prep_certs, dim3(prep_blocks), dim3(256), 0, st, nsigs, nkeys, sig_cert, counts, zero4, status,
+                       ncerts, cert_state);
     const bool tiles = (counts || status) && nsigs > 0;
     const uint32_t nb = std::max<uint32_t>(blocks_for(ncerts, 256), tiles ? blocks_for(nsigs, GROUP_TILE) : 0u);
     if (nb == 0) return hipGetLastError();

@@ -1,4 +1,4 @@
-// One key comb window's verify kernels (k_verify / k_slow_sig for both message modes).
+// One key comb window's verify kernels (k_verify / k_slow_prep for both message modes).
 // Built once per window: -DNW_WA=8, 12, 16, 20 (Makefile).
 #include "nw_verify_kernels.h"
 

@@ -1,4 +1,4 @@
-// k_verify / k_slow_sig templates (one lane per signature).  Instantiated once per key comb window
+// k_verify / k_slow_prep templates (one lane per signature).  Instantiated once per key comb window
 // by nw_kv.hip (compiled with -DNW_WA=8/12/16/20, one object each, so the heavy kernels build in
 // parallel); dispatched by launch_verify / launch_slow in nw_kernels.hip.
 #pragma once
@@ -35,9 +35,15 @@ __device__ __forceinline__ void lane_inputs(const VerifyParams& a, uint32_t i, u
     }
 }
 
-__device__ __forceinline__ void coeff_z(const VerifyParams& a, uint32_t i, uint32_t cert, uint32_t z4[4]) {
-    const uint64_t bidx = a.cert_base + cert;
-    chacha20_z(z4, a.zseed, i - a.cert_first[cert], (uint32_t)bidx, (uint32_t)(bidx >> 32), 0u);
+// A signature whose y does not match R's (so D_i = R_i - P_i != O: it will take the exact batch
+// path) parks its P_i for k_slow_prep, which would otherwise recompute h_i and both combs.  Rare:
+// honest batches never take the branch.
+__device__ __forceinline__ uint32_t park_mismatch(const VerifyParams& a, uint32_t i, const ge_p3& P, uint32_t pf) {
+    if (a.batch_mode && a.pslow && !(pf & PF_YMATCH) && (pf & (NW_F_S_OK | NW_F_A_OK)) == (NW_F_S_OK | NW_F_A_OK)) {
+        store_p3(a.pslow + (size_t)i * 40, P);
+        pf |= NW_F_P_SAVED;
+    }
+    return pf;
 }
 
 // ------------------------------------------------------------------------------------ verify (P_i)
@@ -104,7 +110,7 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     asm volatile("" ::: "memory");
     const uint32_t i2 = a.perm ? a.perm[gid] : gid;
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i2 * 16);
-    store_prec_soa(a.pbuf, a.n, gid, P, verify_pflags(P, R, frow[gid]));
+    store_prec_soa(a.pbuf, a.n, gid, P, park_mismatch(a, i2, P, verify_pflags(P, R, frow[gid])));
 }
 
 // Latency-mode kernel for small launches (nw_verify_split.h, compiled in nw_kvs.hip).
@@ -112,38 +118,72 @@ static constexpr uint32_t VERIFY_SPLIT_MAX_SIGS = 16384;
 template <int WA>
 hipError_t launch_split_wa(const VerifyParams& p, int msgmode, hipStream_t st);
 
-// Exact path for signatures with D_i != O: Q_i = z_i (R_i - P_i); R decode failure -> F_R_BAD.
+// Exact path, step 1 (one lane per entry of the slow list, grid-stride): for a signature whose
+// strict equation fails in a certificate not yet rejected, decode R (failure: F_R_BAD, and the
+// certificate is rejected), form D_i = R_i - P_i and classify it:
+//   SK_SMALL  8 D_i = O, or z_i = 0: then z_i D_i = (z_i mod 8) D_i, summed by k_cert_finalize;
+//   SK_BIG    otherwise: z_i D_i has a nonzero prime-order component (0 < z_i < 2^128 < l).
+// E = <B> (+) E[8] is a direct sum, so a certificate with exactly ONE SK_BIG entry cannot sum to the
+// identity (its prime-order component is z_i D_i' != O) and is rejected without any scalar
+// multiplication; only certificates with two or more SK_BIG entries need z_i D_i (k_slow_mul).
+// Entries of certificates already rejected (bad S / undecodable A, from k_finish) are skipped.
 template <int MSGMODE, int WA>
-__global__ void __launch_bounds__(256) k_slow_sig(VerifyParams a) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= *a.slow_count) return;
-    const uint32_t i = a.slow_list[t];
-    uint32_t* buf = a.slow_buf + (size_t)t * SLOW_WORDS;
-    uint32_t R[8], S[8], h[8], slot, kinfo, cert;
-    lane_inputs<MSGMODE>(a, i, R, S, slot, kinfo, cert, h);
-    ge_p3 Rp;
-    if (!ge_decompress(Rp, R)) {
-        a.flags[i] |= NW_F_R_BAD;
-        store_p3(buf, ge_identity());
-        return;
+__global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
+    const uint32_t cnt = *a.slow_count;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < cnt; t += gridDim.x * blockDim.x) {
+        const uint32_t i = a.slow_list[t];
+        uint32_t* rec = a.slow_buf + (size_t)t * SLOW_WORDS;
+        const uint32_t cert = a.sig_cert[i];
+        if (a.cert_state[cert] & CS_DOOM) {
+            rec[SLOW_KIND] = SK_SKIP;
+            continue;
+        }
+        uint32_t R[8];
+        load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
+        ge_p3 Rp;
+        if (!ge_decompress(Rp, R)) {
+            a.flags[i] |= NW_F_R_BAD;
+            atomicOr(&a.cert_state[cert], CS_DOOM);
+            rec[SLOW_KIND] = SK_SKIP;
+            continue;
+        }
+        ge_p3 P;
+        if (a.flags[i] & NW_F_P_SAVED) {
+            P = load_p3(a.pslow + (size_t)i * 40);
+        } else {   // y matched but x's sign did not (R = -P): recompute P
+            uint32_t R2[8], S[8], h[8], slot, kinfo, c2;
+            lane_inputs<MSGMODE>(a, i, R2, S, slot, kinfo, c2, h);
+            P = compute_P<WA>(S, h, true, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
+        }
+        const ge_p3 D = ge_add(Rp, ge_cached_neg(ge_to_cached(P)));
+        uint32_t z4[4];
+        coeff_z(a, i, cert, z4);
+        const bool zzero = (z4[0] | z4[1] | z4[2] | z4[3]) == 0;
+        const bool small = ge_is_identity(ge_dbl(ge_dbl(ge_dbl(D))));
+        const uint32_t kind = (small || zzero) ? SK_SMALL : SK_BIG;
+        if (kind == SK_BIG) atomicAdd(&a.cert_state[cert], 1u);
+        store_p3(rec, D);
+        rec[SLOW_Z8] = z4[0] & 7u;
+        rec[SLOW_KIND] = kind;
     }
-    const ge_p3 P = compute_P<WA>(S, h, true, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
-    uint32_t z4[4];
-    coeff_z(a, i, cert, z4);
-    store_p3(buf, slow_term(Rp, P, z4));
 }
 
-// Launch k_verify (slow = false, grid over p.gn) or k_slow_sig (slow = true, grid over n_upper).
+// Launch k_verify (slow = false, grid over p.gn) or k_slow_prep (slow = true: a grid-stride grid
+// capped at one 256-thread block per CU, so an honest batch's empty exact path costs one small
+// dispatch whatever n_upper is).
+static constexpr uint32_t SLOW_MAX_BLOCKS = 256;
 template <int WA>
 hipError_t launch_vs_wa(const VerifyParams& p, int msgmode, bool slow, uint32_t n_upper, hipStream_t st) {
     const dim3 b(256);
-    const dim3 g(blocks_for(slow ? n_upper : p.gn, 256));
+    uint32_t nb = blocks_for(slow ? n_upper : p.gn, 256);
+    if (slow && nb > SLOW_MAX_BLOCKS) nb = SLOW_MAX_BLOCKS;
+    const dim3 g(nb);
     if (!slow && p.gn <= VERIFY_SPLIT_MAX_SIGS) return launch_split_wa<WA>(p, msgmode, st);
     if (msgmode == 0) {
-        if (slow) hipLaunchKernelGGL((k_slow_sig<0, WA>), g, b, 0, st, p);
+        if (slow) hipLaunchKernelGGL((k_slow_prep<0, WA>), g, b, 0, st, p);
         else hipLaunchKernelGGL((k_verify<0, WA>), g, b, 0, st, p);
     } else {
-        if (slow) hipLaunchKernelGGL((k_slow_sig<1, WA>), g, b, 0, st, p);
+        if (slow) hipLaunchKernelGGL((k_slow_prep<1, WA>), g, b, 0, st, p);
         else hipLaunchKernelGGL((k_verify<1, WA>), g, b, 0, st, p);
     }
     return hipGetLastError();

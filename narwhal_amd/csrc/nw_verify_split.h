@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
         P = ge_add(P, ge_to_cached(o));
     }
     if (j != 0) return;
-    store_prec_soa(a.pbuf, a.n, gid, P, verify_pflags(P, R, flags));
+    store_prec_soa(a.pbuf, a.n, gid, P, park_mismatch(a, i, P, verify_pflags(P, R, flags)));
 }
 
 template <int WA>
