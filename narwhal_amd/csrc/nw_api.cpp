@@ -20,6 +20,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <random>
 #include <shared_mutex>
 #include <string>
 #include <unordered_map>
@@ -90,6 +91,34 @@ struct HostBuf {
 
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// Key-cache map key: the 32 raw key bytes by value (no per-lookup allocation on the one-message
+// paths), hashed with a per-process random seed so chosen keys cannot pile into one bucket.
+struct Key32 {
+    uint64_t w[4];
+    explicit Key32(const uint8_t* p) { std::memcpy(w, p, 32); }
+    bool operator==(const Key32& o) const {
+        return w[0] == o.w[0] && w[1] == o.w[1] && w[2] == o.w[2] && w[3] == o.w[3];
+    }
+};
+struct Key32Hash {
+    static uint64_t seed() {
+        static const uint64_t s = ((uint64_t)std::random_device{}() << 32) ^ std::random_device{}();
+        return s;
+    }
+    static uint64_t mix(uint64_t x) {   // splitmix64 finalizer
+        x ^= x >> 30;
+        x *= 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 27;
+        x *= 0x94D049BB133111EBull;
+        return x ^ (x >> 31);
+    }
+    size_t operator()(const Key32& k) const {
+        uint64_t h = seed();
+        for (uint64_t v : k.w) h = mix(h ^ v);
+        return (size_t)h;
+    }
+};
+
 // Per-call scratch: one per concurrently executing call.
 struct Workspace {
     hipStream_t stream = nullptr;   // stream of host-buffer calls
@@ -144,7 +173,7 @@ struct nw_ctx {
     uint32_t* d_key_info = nullptr;
     uint32_t* d_stake = nullptr;
     uint32_t* d_key_tab = nullptr;
-    std::unordered_map<std::string, uint32_t> slot_of;
+    std::unordered_map<Key32, uint32_t, Key32Hash> slot_of;
     std::vector<uint32_t> h_stake;
     DevBuf w_bases;               // committee-load scratch (exclusive lock)
     // workspace pool
@@ -373,7 +402,7 @@ int build_keys(nw_ctx* ctx, uint32_t* d_raw, uint32_t* d_info, uint32_t* d_tab, 
 // Slots of keys already in the cache (shared lock held).  Returns true when every key is cached.
 bool lookup_slots(nw_ctx* ctx, const uint8_t (*pk)[32], size_t n, uint32_t* slots) {
     for (size_t i = 0; i < n; ++i) {
-        auto it = ctx->slot_of.find(std::string(reinterpret_cast<const char*>(pk[i]), 32));
+        auto it = ctx->slot_of.find(Key32(pk[i]));
         if (it == ctx->slot_of.end()) return false;
         slots[i] = it->second;
     }
@@ -385,9 +414,9 @@ int ensure_slots(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, si
     std::vector<uint8_t> new_raw;
     std::vector<uint32_t> new_stake;
     std::vector<std::pair<uint32_t, uint32_t>> refresh;   // (slot, stake) of keys already cached
-    std::unordered_map<std::string, uint32_t> pending;
+    std::unordered_map<Key32, uint32_t, Key32Hash> pending;
     for (size_t i = 0; i < n; ++i) {
-        std::string k(reinterpret_cast<const char*>(pk[i]), 32);
+        const Key32 k(pk[i]);
         auto it = ctx->slot_of.find(k);
         if (it != ctx->slot_of.end()) {
             slots[i] = it->second;
@@ -438,13 +467,48 @@ int ensure_slots(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, si
     return NW_OK;
 }
 
+// Preamble state a small host-buffer call uploads with its inputs (one DMA), so the batch starts
+// with no preamble kernels: the vote -> certificate map (host-expanded), the zeroed slow-path
+// counter and the zeroed per-certificate exact-path state.
+struct PreStaged {
+    uint32_t* sig_cert;     // [nsigs + 1]
+    uint32_t* zero4;        // [4]
+    uint32_t* cert_state;   // [ncerts]
+};
+// Calls below this many signatures (and whose staged bytes fit kDirectCopyBytes) use PreStaged:
+// the signer grouping (k_expand_count's histogram) only runs from kGroupMinSigs up.
+constexpr size_t kStagedMaxSigs = 16384;
+static_assert(kStagedMaxSigs <= kGroupMinSigs, "staged calls never group");
+
+// Bytes of the PreStaged block for a call (256-B aligned segments).
+size_t prestaged_bytes(size_t nsigs, size_t ncerts) {
+    return align256((nsigs + 1) * 4) + 256 + align256(ncerts * 4 + 4);
+}
+
+// Fill the PreStaged block at h (host staging) and point pre at the same offsets from d.
+void prestage(uint8_t* h, uint8_t* d, const uint32_t* first, const uint32_t* nv, size_t ncerts, size_t nsigs,
+              PreStaged& pre) {
+    const size_t o_sc = 0, o_z = align256((nsigs + 1) * 4), o_cs = o_z + 256;
+    uint32_t* sc = reinterpret_cast<uint32_t*>(h + o_sc);
+    std::memset(h, 0, prestaged_bytes(nsigs, ncerts));
+    for (size_t c = 0; c < ncerts; ++c) {   // host-validated ranges: inside [0, nsigs)
+        const size_t f = first[c], e = f + nv[c];
+        for (size_t v = f; v < e; ++v) sc[v] = (uint32_t)c;
+    }
+    pre.sig_cert = reinterpret_cast<uint32_t*>(d + o_sc);
+    pre.zero4 = reinterpret_cast<uint32_t*>(d + o_z);
+    pre.cert_state = reinterpret_cast<uint32_t*>(d + o_cs);
+}
+
 // Enqueue the certificate pipeline on device buffers (shared key lock held, workspace bound to st).
+// With ``pre`` the preamble state is already in device memory (small host-buffer calls).  A strict
+// call's verdict bytes (d_sig_ok, batch_mode 0) come straight from k_finish.
 int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_first, const uint32_t* d_nv,
                   size_t nsigs, const uint8_t* d_sig, const uint32_t* d_signer, int msgmode, const uint8_t* d_msg32,
                   const uint8_t* d_msg_base, const uint64_t* d_msg_off, const uint64_t* d_msg_len,
                   const uint8_t* zseed, uint64_t cert_base, uint32_t batch_mode, uint8_t* d_cert_ok,
                   uint32_t* d_flags_user, uint64_t* d_stake_out, hipStream_t st, uint8_t* d_sig_ok = nullptr,
-                  uint32_t* d_status = nullptr) {
+                  uint32_t* d_status = nullptr, const PreStaged* pre = nullptr) {
     uint32_t* d_flags = d_flags_user;
     if (!d_flags) {
         NW_TRY(ws->ensure(ws->w_flags, nsigs * 4 + 4), "ws flags");
@@ -462,28 +526,32 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     NW_TRY(ws->ensure(ws->w_pbuf, nsigs * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
     NW_TRY(ws->ensure(ws->w_pre, nsigs * 40 + 16), "ws pre");
     // signer grouping (device counting sort) when keys repeat
-    const bool group = !ctx->group_off && nsigs >= kGroupMinSigs && ctx->nkeys > 1 &&
+    const bool group = !pre && !ctx->group_off && nsigs >= kGroupMinSigs && ctx->nkeys > 1 &&
                        nsigs >= kGroupMinSigsPerKey * ctx->nkeys;
     if (group) {
         NW_TRY(ws->ensure(ws->w_counts, ctx->nkeys * 4 + 16), "ws counts");
         NW_TRY(ws->ensure(ws->w_cursor, ctx->nkeys * 4 + 16), "ws cursor");
         NW_TRY(ws->ensure(ws->w_perm, nsigs * 4 + 16), "ws perm");
     }
-    // Preamble in two launches: zero sig_cert (votes outside every certificate map to certificate
-    // 0), the slot counts, the slow-path counter and d_status; expand certificates; histogram
-    // signer slots; check the device inputs into d_status (when given).
-    NW_TRY(launch_prep_expand((uint32_t)ncerts, (uint32_t)nsigs, (uint32_t)ctx->nkeys, d_first, d_nv, d_signer,
-                              ws->w_sig_cert.as<uint32_t>(), ws->w_slow_count.as<uint32_t>(),
-                              group ? ws->w_counts.as<uint32_t>() : nullptr, d_status,
-                              batch_mode ? ws->w_cert_state.as<uint32_t>() : nullptr, st),
-           "k_prep_certs / k_expand_count");
+    uint32_t* sig_cert = pre ? pre->sig_cert : ws->w_sig_cert.as<uint32_t>();
+    uint32_t* slow_count = pre ? pre->zero4 : ws->w_slow_count.as<uint32_t>();
+    uint32_t* cert_state = !batch_mode ? nullptr : (pre ? pre->cert_state : ws->w_cert_state.as<uint32_t>());
+    if (!pre) {
+        // Preamble in two launches: zero sig_cert (votes outside every certificate map to certificate
+        // 0), the slot counts, the slow-path counter, the certificate states and d_status; expand
+        // certificates; histogram signer slots; check the device inputs into d_status (when given).
+        NW_TRY(launch_prep_expand((uint32_t)ncerts, (uint32_t)nsigs, (uint32_t)ctx->nkeys, d_first, d_nv, d_signer,
+                                  sig_cert, slow_count, group ? ws->w_counts.as<uint32_t>() : nullptr, d_status,
+                                  cert_state, st),
+               "k_prep_certs / k_expand_count");
+    }
 
     VerifyParams vp{};
     vp.n = (uint32_t)nsigs;
     vp.batch_mode = batch_mode;
     vp.sig = d_sig;
     vp.signer = d_signer;
-    vp.sig_cert = ws->w_sig_cert.as<uint32_t>();
+    vp.sig_cert = sig_cert;
     vp.cert_first = d_first;
     vp.cert_msg = d_msg32;
     vp.msg_base = d_msg_base;
@@ -498,12 +566,13 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     static const uint8_t kNoSeed[32] = {0};   // strict-only calls draw no coefficients
     std::memcpy(vp.zseed, zseed ? zseed : kNoSeed, 32);
     vp.flags = d_flags;
-    vp.slow_count = ws->w_slow_count.as<uint32_t>();
+    vp.slow_count = slow_count;
     vp.slow_list = ws->w_slow_list.as<uint32_t>();
     vp.slow_slot = ws->w_slow_slot.as<uint32_t>();
     vp.slow_buf = ws->w_slow_buf.as<uint32_t>();
     vp.pslow = batch_mode ? ws->w_pslow.as<uint32_t>() : nullptr;
-    vp.cert_state = batch_mode ? ws->w_cert_state.as<uint32_t>() : nullptr;
+    vp.cert_state = cert_state;
+    vp.ok_out = batch_mode ? nullptr : d_sig_ok;
     vp.pbuf = ws->w_pbuf.as<uint32_t>();
     vp.pre = ws->w_pre.as<uint32_t>();
     vp.perm = nullptr;
@@ -535,10 +604,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     NW_TRY(launch_verify(vp, msgmode, ctx->key_window, st), "k_verify");
     if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");   // brackets k_verify alone
     NW_TRY(launch_finish(vp, st), "k_finish");
-    if (!batch_mode) {   // strict verdicts only: no certificate pass
-        if (d_sig_ok) NW_TRY(launch_flags_to_ok((uint32_t)nsigs, d_flags, d_sig_ok, st), "k_flags_to_ok");
-        return NW_OK;
-    }
+    if (!batch_mode) return NW_OK;   // strict verdicts only (bytes written by k_finish): no certificate pass
 
     NW_TRY(launch_slow(vp, msgmode, ctx->key_window, (uint32_t)nsigs, st), "k_slow_prep / k_slow_mul");
 
@@ -639,7 +705,7 @@ int upload_messages(nw_ctx* ctx, Workspace* ws, Stager& sg, const uint8_t* const
 
 // Strict verify of signatures whose keys are not cached: k_verify_var + k_finish (messages, sigs
 // and raw keys already uploaded to the workspace).
-int enqueue_strict_var(nw_ctx* ctx, Workspace* ws, size_t n, hipStream_t st) {
+int enqueue_strict_var(nw_ctx* ctx, Workspace* ws, size_t n, hipStream_t st, uint8_t* d_ok = nullptr) {
     NW_TRY(ws->ensure(ws->w_flags, n * 4 + 4), "ws flags");
     NW_TRY(ws->ensure(ws->w_sig_cert, n * 4 + 4), "ws sig_cert");
     NW_TRY(ws->ensure(ws->w_pbuf, n * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
@@ -662,6 +728,7 @@ int enqueue_strict_var(nw_ctx* ctx, Workspace* ws, size_t n, hipStream_t st) {
     vp.flags = ws->w_flags.as<uint32_t>();
     vp.pbuf = ws->w_pbuf.as<uint32_t>();
     vp.pre = ws->w_pre.as<uint32_t>();
+    vp.ok_out = d_ok;   // verdict bytes straight from k_finish
     NW_TRY(launch_verify_var(vp, 1, ws->w_var.as<uint32_t>(), st), "k_verify_var");
     NW_TRY(launch_finish(vp, st), "k_finish");
     return NW_OK;
@@ -768,6 +835,13 @@ int upload_sig_keys(nw_ctx* ctx, Workspace* ws, const uint8_t* const* msg, const
     return NW_OK;
 }
 
+// Staged bytes of run_generic's one-DMA layout (messages, offsets, lengths, sigs, slots, the
+// certificate word pair and the preamble state).
+size_t packed_bytes(size_t total, size_t n) {
+    return align256(total + 8) + 2 * align256(n * 8) + align256(n * 64) + align256(n * 4) + 256 +
+           prestaged_bytes(n, 1);
+}
+
 // Shared body of strict_many / verify_batch: every signature in one "certificate" 0.  Cached keys
 // take the comb path; a call with any key outside the cache takes the variable-base path (strict:
 // k_verify_var; batch: the MSM) and leaves the cache unchanged.
@@ -797,9 +871,55 @@ int run_generic(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const
                              st);
             if (rc != NW_OK) return rc;
         } else {
-            rc = enqueue_strict_var(ctx, ws, n, st);
+            rc = enqueue_strict_var(ctx, ws, n, st, ws->w_ok.as<uint8_t>());
             if (rc != NW_OK) return rc;
         }
+    } else if (n <= kStagedMaxSigs && packed_bytes(message_bytes(len, n), n) < kDirectCopyBytes) {
+        // one-message paths (Signature::verify, one certificate's verify_batch): every input and the
+        // preamble state in ONE staged H2D, no preamble kernels, both outputs in ONE D2H
+        const size_t total = message_bytes(len, n);
+        const size_t o_msg = 0, o_off = align256(total + 8), o_len = o_off + align256(n * 8),
+                     o_sig = o_len + align256(n * 8), o_signer = o_sig + align256(n * 64),
+                     o_fn = o_signer + align256(n * 4), o_pre = o_fn + 256,
+                     in_bytes = o_pre + prestaged_bytes(n, 1);
+        const size_t o_cok = 0, o_ok = 256, out_bytes = align256(256 + n);
+        NW_TRY(ws->ensure(ws->w_io, in_bytes + out_bytes), "ws io");
+        NW_TRY(ws->h_io.ensure(in_bytes > out_bytes ? in_bytes : out_bytes), "pinned io");
+        uint8_t* h = ws->h_io.bytes();
+        uint8_t* d = ws->w_io.as<uint8_t>();
+        uint8_t* d_out = d + in_bytes;
+        uint64_t* hoff = reinterpret_cast<uint64_t*>(h + o_off);
+        uint64_t* hlen = reinterpret_cast<uint64_t*>(h + o_len);
+        size_t pos = 0;
+        for (size_t i = 0; i < n; ++i) {
+            hoff[i] = pos;
+            hlen[i] = len[i];
+            if (len[i]) std::memcpy(h + o_msg + pos, msg[i], len[i]);
+            pos += len[i];
+        }
+        std::memset(h + o_msg + pos, 0, 8);
+        std::memcpy(h + o_sig, sig, n * 64);
+        std::memcpy(h + o_signer, slots.data(), n * 4);
+        uint32_t* fn = reinterpret_cast<uint32_t*>(h + o_fn);
+        fn[0] = 0;
+        fn[1] = (uint32_t)n;
+        PreStaged pre{};
+        prestage(h + o_pre, d + o_pre, fn, fn + 1, 1, n, pre);
+        NW_TRY(hipMemcpyAsync(d, h, in_bytes, hipMemcpyHostToDevice, st), "H2D inputs");
+        rc = enqueue_certs(ctx, ws, 1, reinterpret_cast<const uint32_t*>(d + o_fn),
+                           reinterpret_cast<const uint32_t*>(d + o_fn + 4), n, d + o_sig,
+                           reinterpret_cast<const uint32_t*>(d + o_signer), 1, nullptr, d + o_msg,
+                           reinterpret_cast<const uint64_t*>(d + o_off), reinterpret_cast<const uint64_t*>(d + o_len),
+                           zseed, batch_index, batch_mode, d_out + o_cok, nullptr, nullptr, st,
+                           ok_out ? d_out + o_ok : nullptr, nullptr, &pre);
+        if (rc != NW_OK) return rc;
+        // the H2D above has completed in stream order before this copy overwrites the staging buffer
+        NW_TRY(hipMemcpyAsync(h, d_out, out_bytes, hipMemcpyDeviceToHost, st), "D2H outputs");
+        NW_TRY(hipStreamSynchronize(st), "sync");
+        lease.synced();
+        if (ok_out) std::memcpy(ok_out, h + o_ok, n);
+        if (verdict_out) *verdict_out = h[o_cok];
+        return NW_OK;
     } else {
         const size_t total = message_bytes(len, n);
         Stager sg(ws, st);
@@ -825,12 +945,7 @@ int run_generic(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const
                            ok_out ? ws->w_ok.as<uint8_t>() : nullptr);   // verdict bytes from k_cert_finalize
         if (rc != NW_OK) return rc;
     }
-    if (ok_out) {
-        if (!cached)
-            NW_TRY(launch_flags_to_ok((uint32_t)n, ws->w_flags.as<uint32_t>(), ws->w_ok.as<uint8_t>(), st),
-                   "k_flags_to_ok");
-        NW_TRY(hipMemcpyAsync(ok_out, ws->w_ok.p, n, hipMemcpyDeviceToHost, st), "D2H ok");
-    }
+    if (ok_out) NW_TRY(hipMemcpyAsync(ok_out, ws->w_ok.p, n, hipMemcpyDeviceToHost, st), "D2H ok");
     if (verdict_out) NW_TRY(hipMemcpyAsync(verdict_out, ws->w_cert_ok.p, 1, hipMemcpyDeviceToHost, st), "D2H");
     NW_TRY(hipStreamSynchronize(st), "sync");
     lease.synced();
@@ -1130,9 +1245,11 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
     // one D2H.  Large calls: the signature and signer arrays go straight from the caller's pageable
     // buffers (see kDirectCopyBytes).
     const bool direct = nsigs * 64 >= kDirectCopyBytes;
+    const bool staged = !direct && nsigs <= kStagedMaxSigs;   // preamble state rides along: no preamble kernels
     const size_t o_sig = 0, o_signer = align256(o_sig + nsigs * 64), o_first = align256(o_signer + nsigs * 4),
                  o_nv = align256(o_first + ncerts * 4), o_msg = align256(o_nv + ncerts * 4),
-                 in_bytes = align256(o_msg + ncerts * 32);
+                 o_pre = align256(o_msg + ncerts * 32),
+                 in_bytes = o_pre + (staged ? prestaged_bytes(nsigs, ncerts) : 0);
     const size_t o_cok = 0, o_stake = align256(ncerts), o_ok = align256(o_stake + ncerts * 8),
                  out_bytes = align256(o_ok + nsigs);
     NW_TRY(ws->ensure(ws->w_io, in_bytes + out_bytes), "ws io");
@@ -1147,6 +1264,8 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
     std::memcpy(h + o_first, first.data(), ncerts * 4);
     std::memcpy(h + o_nv, nv.data(), ncerts * 4);
     std::memcpy(h + o_msg, msg, ncerts * 32);
+    PreStaged pre{};
+    if (staged) prestage(h + o_pre, d_in + o_pre, first.data(), nv.data(), ncerts, nsigs, pre);
     if (direct) {
         NW_TRY(hipMemcpyAsync(d_in + o_sig, sig, nsigs * 64, hipMemcpyHostToDevice, st), "H2D sig");
         NW_TRY(hipMemcpyAsync(d_in + o_signer, signer_slot, nsigs * 4, hipMemcpyHostToDevice, st), "H2D signer");
@@ -1159,7 +1278,8 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
                            reinterpret_cast<const uint32_t*>(d_in + o_nv), nsigs, d_in + o_sig,
                            reinterpret_cast<const uint32_t*>(d_in + o_signer), 0, d_in + o_msg, nullptr, nullptr,
                            nullptr, zseed, cert_base, 1, d_out + o_cok, nullptr,
-                           reinterpret_cast<uint64_t*>(d_out + o_stake), st, sig_ok && nsigs ? d_out + o_ok : nullptr);
+                           reinterpret_cast<uint64_t*>(d_out + o_stake), st, sig_ok && nsigs ? d_out + o_ok : nullptr,
+                           nullptr, staged ? &pre : nullptr);
     if (rc != NW_OK) return rc;   // the lease synchronizes the stream (the H2D may be in flight)
     // the H2D above has completed in stream order before this copy overwrites the staging buffer
     NW_TRY(hipMemcpyAsync(h, d_out, out_bytes, hipMemcpyDeviceToHost, st), "D2H outputs");

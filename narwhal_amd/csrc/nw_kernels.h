@@ -61,6 +61,7 @@ struct VerifyParams {
     uint32_t* slow_buf;            // [n][SLOW_WORDS]
     uint32_t* pslow;               // [n][40] P_i of signatures whose y did not match (batch mode; may be null)
     uint32_t* cert_state;          // [ncerts] CS_* exact-path state (batch mode)
+    uint8_t* ok_out;               // [n] strict verdict bytes written by k_finish (strict calls; may be null)
     uint32_t* pbuf;                // [PREC_ROWS][n] SoA, processing order: P's X, Z + partial flags
     uint32_t* pre;                 // [10][n] SoA prefix products of Z (k_finish scratch)
     const uint32_t* perm;          // [n] processing order for k_verify (signer-grouped) or null

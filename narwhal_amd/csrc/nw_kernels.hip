@@ -134,8 +134,10 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
     // divsteps for one signature per lane (latency-bound launches: with 64 independent inversions
     // per wave the variable-time loop runs the slowest lane's count, measured 10% slower there:
     // profiles/r02/ab_r02.txt).  a.fk is uniform, so the branch does not diverge.
+    // A launch of a handful of signatures (one header / vote signature) has a handful of active
+    // lanes, so the variable-time loop's cost is that one lane's own count: variable time again.
     fe inv;
-    if (NW_INV_VAR && a.fk >= 4) inv = fe_invert_var(acc);
+    if (NW_INV_VAR && (a.fk >= 4 || a.gn <= 8)) inv = fe_invert_var(acc);
     else inv = fe_invert_sg(acc);
 #pragma unroll
     for (int k = FINISH_K - 1; k >= 0; --k) {
@@ -161,6 +163,7 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
                 }
             }
             a.flags[i] = f;
+            if (a.ok_out) a.ok_out[i] = (f & NW_F_STRICT) ? 1 : 0;
         }
     }
 }

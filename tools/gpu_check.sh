@@ -32,4 +32,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format c
 grep '^{' $OUT/onecall.log
 python3 tools/one_call_trace.py --analyze $OUT/prof_onecall > $OUT/onecall_anatomy.txt 2>&1; tail -12 $OUT/onecall_anatomy.txt | cut -c1-600
 fi
+if [ -n "$CONFIGS" ]; then
+timeout -k 10 600 python3 -u tools/bench_configs.py --only $CONFIGS --cpu-seconds 0 > $OUT/configs.jsonl 2> $OUT/configs.err || { echo "CONFIGS FAILED"; tail -20 $OUT/configs.err; exit 1; }
+cut -c1-400 $OUT/configs.jsonl
+fi
+if [ -n "$PROF_CONFIG" ]; then
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_cfg -o cfg -- python3 tools/bench_configs.py --only $PROF_CONFIG --cpu-seconds 0 --steps 3 > $OUT/prof_cfg.log 2>&1 || { echo "PROF CONFIG FAILED"; tail -20 $OUT/prof_cfg.log; exit 1; }
+f=$(find $OUT/prof_cfg -name '*kernel_stats.csv' | head -1)
+[ -n "$f" ] && cp "$f" $OUT/kernel_stats_cfg.csv && cut -d, -f1-4 $OUT/kernel_stats_cfg.csv | cut -c1-150 | head -24
+fi
 exit 0
