@@ -9,7 +9,7 @@ import ed25519_oracle as o
 import vectors
 
 L = o.L
-CLASSES = ["ii", "iii", "v", "vi", "vii", "viii", "ix"]
+CLASSES = ["ii", "iii", "v", "vi", "vii", "viii", "ix"]   # signature-level; key-level: add_torsion_members
 
 
 def secret_scalar(seed: bytes):
@@ -70,3 +70,52 @@ def make_adversarial(cs, com, frac: float, rng: np.random.Generator):
         sigs[i] = np.frombuffer(bytes(s), np.uint8)
     cs.sigs = sigs
     return kinds
+
+
+def add_torsion_members(cs, com, members_small, members_mixed):
+    """Key-level classes at committee scale: committee members whose cached keys carry a torsion
+    component.  Every vote of a member in ``members_small`` is re-signed under a small-order key
+    A = T (class i: R = rB, S = r, so the batch residual h T is pure torsion); every vote of a member
+    in ``members_mixed`` under the mixed-order key A' = aB + jT8 with the member's own scalar
+    (class iv: honest R, S' = r + H(R||A'||M) a).  The nonce r of each vote is recovered from its
+    honest signature (r = S - H(R||A||M) a mod l), so no point arithmetic runs per vote.
+    Returns (committee with the torsion keys appended, {signature index: class}); ``cs.signer``
+    and ``cs.sigs`` are rewritten in place to point at the appended keys."""
+    import copy
+    t8 = o.small_order_generator()
+    small = [p for p in o.small_order_points() if not o.pt_is_identity(p)]
+    new_pks, new_seeds, kinds = [], [], {}
+    sigs = cs.sigs.copy()
+    signer = cs.signer.copy()
+    cert_of = np.repeat(np.arange(cs.ncerts), cs.cert_n.astype(np.int64))
+    base = com.size
+    for j, (mem, cls) in enumerate([(m, "i") for m in members_small] + [(m, "iv") for m in members_mixed]):
+        seed = bytes(com.seeds[mem])
+        a, _ = secret_scalar(seed)
+        pk = bytes(com.pks[mem])
+        if cls == "i":
+            A2 = o.pt_compress(small[j % len(small)])
+        else:
+            A2 = o.pt_compress(o.pt_add(o.pt_mul(a, o.B_POINT), o.pt_mul(1 + 2 * (j % 4), t8)))
+        new_pks.append(np.frombuffer(A2, np.uint8))
+        new_seeds.append(com.seeds[mem])
+        slot = base + j
+        for i in np.nonzero(cs.signer == mem)[0]:
+            msg = bytes(cs.msgs[cert_of[i]])
+            R, S = bytes(sigs[i][:32]), int.from_bytes(bytes(sigs[i][32:]), "little")
+            k = int.from_bytes(hashlib.sha512(R + pk + msg).digest(), "little") % L
+            r = (S - k * a) % L
+            if cls == "i":
+                s2 = r
+            else:
+                k2 = int.from_bytes(hashlib.sha512(R + A2 + msg).digest(), "little") % L
+                s2 = (r + k2 * a) % L
+            sigs[i] = np.frombuffer(R + s2.to_bytes(32, "little"), np.uint8)
+            signer[i] = slot
+            kinds[int(i)] = cls
+    cs.sigs, cs.signer = sigs, signer
+    com2 = copy.copy(com)
+    com2.pks = np.concatenate([com.pks, np.stack(new_pks)])
+    com2.seeds = np.concatenate([com.seeds, np.stack(new_seeds)])
+    com2.stake = np.concatenate([com.stake, np.ones(len(new_pks), com.stake.dtype)])
+    return com2, kinds

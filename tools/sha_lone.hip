@@ -1,0 +1,258 @@
+// Lone-chain SHA-512 microbenchmark: where do the cycles of one long message go?
+//
+// One workgroup, one message (every lane computes the same chain; a wave's issue cost does not
+// depend on its active lanes).  Each variant runs NB compressions back to back and stamps
+// s_memtime (shader clock) and s_memrealtime (100 MHz) around them, so cycles per round and
+// ns per block are read off independently of the clock the GPU picks.
+//   rounds_reg  : the 80 rounds with K_t + W_t from registers (no LDS, no schedule): the round
+//                 code's own issue + dependency cost
+//   rounds_lds  : the same with K_t + W_t read from LDS 16 words ahead (the split kernel's round wave)
+//   full_inline : message schedule inline (k_sha512_many's form), block from global memory
+//   two_lane    : e-chain on even lanes, a-chain on odd lanes (nw_sha512_2l.h): Sigma and Ch/Maj
+//                 computed once for both chains, one cross-lane exchange per round
+// Build: hipcc -O3 --offload-arch=gfx950 -I narwhal_amd/csrc tools/sha_lone.hip -o tools/sha_lone
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+#include "nw_sha512.h"
+#include "nw_sha512_2l.h"
+#include "nw_digest.hip"   // k_sha512_split / k_sha512_split2 / k_sha512_many as shipped
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+    fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); return 1; } } while (0)
+
+using namespace nw;
+
+#define NW_R(a, b, c, d, e, f, g, h, kw)                                                               \
+    do {                                                                                                \
+        const uint64_t t1 = (h) + (kw) + xor3_64(rotr64((e), 14), rotr64((e), 18), rotr64((e), 41)) +     \
+                            ch64((e), (f), (g));                                                        \
+        const uint64_t t2 = xor3_64(rotr64((a), 28), rotr64((a), 34), rotr64((a), 39)) + maj64((a), (b), (c)); \
+        (d) += t1;                                                                                      \
+        (h) = t1 + t2;                                                                                  \
+    } while (0)
+
+#define NW_R16(KW)                                                                                    \
+    NW_R(a, b, c, d, e, f, g, h, KW[0]);  NW_R(h, a, b, c, d, e, f, g, KW[1]);                           \
+    NW_R(g, h, a, b, c, d, e, f, KW[2]);  NW_R(f, g, h, a, b, c, d, e, KW[3]);                           \
+    NW_R(e, f, g, h, a, b, c, d, KW[4]);  NW_R(d, e, f, g, h, a, b, c, KW[5]);                           \
+    NW_R(c, d, e, f, g, h, a, b, KW[6]);  NW_R(b, c, d, e, f, g, h, a, KW[7]);                           \
+    NW_R(a, b, c, d, e, f, g, h, KW[8]);  NW_R(h, a, b, c, d, e, f, g, KW[9]);                           \
+    NW_R(g, h, a, b, c, d, e, f, KW[10]); NW_R(f, g, h, a, b, c, d, e, KW[11]);                          \
+    NW_R(e, f, g, h, a, b, c, d, KW[12]); NW_R(d, e, f, g, h, a, b, c, KW[13]);                          \
+    NW_R(c, d, e, f, g, h, a, b, KW[14]); NW_R(b, c, d, e, f, g, h, a, KW[15]);
+
+__device__ __forceinline__ void stamp(uint64_t* t, int k) {
+    t[2 * k] = __builtin_amdgcn_s_memtime();
+    t[2 * k + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
+// K_t + W_t for one fixed block, in registers; the chaining state is carried across NB blocks
+__global__ void __launch_bounds__(64) k_rounds_reg(uint32_t nb, const uint64_t* kwin, uint64_t* out, uint64_t* ts) {
+    uint64_t kw[80];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) kw[t] = kwin[t];
+    uint64_t st[8];
+    sha512_init(st);
+    uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t blk = 0; blk < nb; ++blk) {
+        uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+        NW_R16((kw + 0)) NW_R16((kw + 16)) NW_R16((kw + 32)) NW_R16((kw + 48)) NW_R16((kw + 64))
+        st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+    }
+    uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 8; ++i) out[i] = st[i];
+        ts[0] = t1 - t0; ts[1] = r1 - r0;
+    }
+}
+
+__global__ void __launch_bounds__(64) k_rounds_lds(uint32_t nb, const uint64_t* kwin, uint64_t* out, uint64_t* ts) {
+    __shared__ uint64_t kwb[80][64];
+    const uint32_t lane = threadIdx.x;
+    for (int t = 0; t < 80; ++t) kwb[t][lane] = kwin[t];
+    __syncthreads();
+    uint64_t st[8];
+    sha512_init(st);
+    uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t blk = 0; blk < nb; ++blk) {
+        uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+        uint64_t k0[16], k1[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) k0[q] = kwb[q][lane];
+#pragma unroll
+        for (int grp = 0; grp < 5; ++grp) {
+            if (grp < 4) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) k1[q] = kwb[(grp + 1) * 16 + q][lane];
+            }
+            NW_R16(k0)
+            if (grp < 4) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) k0[q] = k1[q];
+            }
+        }
+        st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+    }
+    uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 8; ++i) out[i] = st[i];
+        ts[0] = t1 - t0; ts[1] = r1 - r0;
+    }
+}
+
+// k_sha512_many's loop body: block words from global memory, schedule inline
+__global__ void __launch_bounds__(64) k_full_inline(uint32_t nb, const uint64_t* blocks, uint64_t* out, uint64_t* ts) {
+    uint64_t st[8];
+    sha512_init(st);
+    uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t blk = 0; blk < nb; ++blk) {
+        uint64_t w[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = blocks[(size_t)(blk & 1023) * 16 + i];
+        sha512_compress(st, w);
+    }
+    uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 8; ++i) out[i] = st[i];
+        ts[0] = t1 - t0; ts[1] = r1 - r0;
+    }
+}
+
+// two-lane form with K_t + W_t from registers (kwlane[t][lane]: K_t + W_t on even lanes, 1 on odd)
+__global__ void __launch_bounds__(64) k_two_lane(uint32_t nb, const uint64_t* kwlane, uint64_t* out, uint64_t* ts) {
+    const uint32_t lane = threadIdx.x;
+    const bool odd = lane & 1;
+    uint64_t kw[80];
+#pragma unroll
+    for (int t = 0; t < 80; ++t) kw[t] = kwlane[t * 64 + lane];
+    uint64_t h[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) h[i] = SHA512_IV[(odd ? 0 : 4) + i];
+    Sha2L s2;
+    s2.init(odd);
+    uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t blk = 0; blk < nb; ++blk) s2.block(h, [&](int t) { return kw[t]; });
+    uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (lane < 2) {
+        for (int i = 0; i < 4; ++i) out[(odd ? 0 : 4) + i] = h[i];
+        if (lane == 0) { ts[0] = t1 - t0; ts[1] = r1 - r0; }
+    }
+}
+
+// host reference: nb compressions of the fixed (K + W) schedule
+static void host_rounds(uint32_t nb, const uint64_t* kw, uint64_t st[8]) {
+    for (int i = 0; i < 8; ++i) st[i] = SHA512_IV[i];
+    for (uint32_t blk = 0; blk < nb; ++blk) {
+        uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+        for (int t = 0; t < 80; ++t) {
+            const uint64_t t1 = h + kw[t] + (rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41)) + ((e & f) ^ (~e & g));
+            const uint64_t t2 = (rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
+            h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        }
+        st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+    }
+}
+
+int main(int argc, char** argv) {
+    const uint32_t nb = argc > 1 ? (uint32_t)atoi(argv[1]) : 2000;
+    std::vector<uint64_t> kw(80), blocks(1024 * 16);
+    for (int t = 0; t < 80; ++t) kw[t] = SHA512_K[t] ^ (0x9E3779B97F4A7C15ull * (t + 1));
+    for (size_t i = 0; i < blocks.size(); ++i) blocks[i] = 0x0123456789ABCDEFull * (i + 7);
+    std::vector<uint64_t> kwl(80 * 64);
+    for (int t = 0; t < 80; ++t)
+        for (int l = 0; l < 64; ++l) kwl[t * 64 + l] = (l & 1) ? 1ull : kw[t];
+    uint64_t *d_kw, *d_kwl, *d_blocks, *d_out, *d_ts;
+    CHECK(hipMalloc(&d_kw, 80 * 8));
+    CHECK(hipMalloc(&d_kwl, kwl.size() * 8));
+    CHECK(hipMemcpy(d_kwl, kwl.data(), kwl.size() * 8, hipMemcpyHostToDevice));
+    CHECK(hipMalloc(&d_blocks, blocks.size() * 8));
+    CHECK(hipMalloc(&d_out, 64));
+    CHECK(hipMalloc(&d_ts, 16));
+    CHECK(hipMemcpy(d_kw, kw.data(), 80 * 8, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(d_blocks, blocks.data(), blocks.size() * 8, hipMemcpyHostToDevice));
+    uint64_t ref[8];
+    host_rounds(nb, kw.data(), ref);
+    struct V { const char* name; void (*k)(uint32_t, const uint64_t*, uint64_t*, uint64_t*); const uint64_t* in; bool reg_ref; };
+    V vs[] = {{"rounds_reg", k_rounds_reg, d_kw, true}, {"rounds_lds", k_rounds_lds, d_kw, true},
+              {"full_inline", k_full_inline, d_blocks, false}, {"two_lane", k_two_lane, d_kwl, true}};
+    for (const V& v : vs) {
+        for (int rep = 0; rep < 3; ++rep) {
+            hipLaunchKernelGGL(v.k, dim3(1), dim3(64), 0, 0, nb, v.in, d_out, d_ts);
+            CHECK(hipDeviceSynchronize());
+        }
+        uint64_t ts[2], out[8];
+        CHECK(hipMemcpy(ts, d_ts, 16, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(out, d_out, 64, hipMemcpyDeviceToHost));
+        const bool ok = !v.reg_ref || memcmp(out, ref, 64) == 0;
+        const double ns = ts[1] * 10.0;   // s_memrealtime: 100 MHz
+        printf("{\"variant\": \"%s\", \"blocks\": %u, \"cyc_per_round\": %.1f, \"ns_per_block\": %.1f, "
+               "\"clock_ghz\": %.3f, \"matches_host\": %s}\n",
+               v.name, nb, (double)ts[0] / nb / 80.0, ns / nb, ts[0] / ns, ok ? "true" : "false");
+    }
+    // the shipped kernels on ONE message of nb * 128 - 17 bytes (nb blocks with the padding)
+    const uint64_t L = (uint64_t)nb * 128 - 17;
+    uint8_t* d_msg;
+    uint64_t *d_off, *d_len;
+    uint8_t* d_dig;
+    CHECK(hipMalloc(&d_msg, L + 64));
+    CHECK(hipMalloc(&d_off, 8));
+    CHECK(hipMalloc(&d_len, 8));
+    CHECK(hipMalloc(&d_dig, 64 * 3));
+    CHECK(hipMemset(d_msg, 0x5A, L));
+    const uint64_t zero = 0;
+    CHECK(hipMemcpy(d_off, &zero, 8, hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(d_len, &L, 8, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    const char* names[3] = {"k_sha512_split", "k_sha512_split2", "k_sha512_many"};
+    // the same message at the far end of a 4 GiB buffer (the bench's 10,000 worker batches are one
+    // 5 GB tensor): fresh pages / TLB reach
+    uint8_t* d_big;
+    const size_t big = (size_t)4 << 30;
+    CHECK(hipMalloc(&d_big, big));
+    CHECK(hipMemset(d_big, 0x5A, big));
+    const uint64_t far_off = (uint64_t)(big - L - 64) & ~(uint64_t)127;
+    uint64_t* d_off_far;
+    CHECK(hipMalloc(&d_off_far, 8));
+    CHECK(hipMemcpy(d_off_far, &far_off, 8, hipMemcpyHostToDevice));
+    for (int k = 0; k < 2; ++k) {
+        float best = 1e30f;
+        for (int rep = 0; rep < 3; ++rep) {
+            CHECK(hipEventRecord(e0, 0));
+            if (k == 0) hipLaunchKernelGGL(k_sha512_split, dim3(1), dim3(128), 0, 0, 1u, d_big, d_off_far, d_len, d_dig);
+            else hipLaunchKernelGGL(k_sha512_split2, dim3(1), dim3(128), 0, 0, 1u, d_big, d_off_far, d_len, d_dig + 64);
+            CHECK(hipEventRecord(e1, 0));
+            CHECK(hipEventSynchronize(e1));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            best = ms < best ? ms : best;
+        }
+        printf("{\"kernel\": \"%s\", \"where\": \"end of a 4 GiB buffer\", \"blocks\": %u, \"ms\": %.3f, "
+               "\"ns_per_block\": %.1f}\n", names[k], nb, best, best * 1e6 / nb);
+    }
+    CHECK(hipFree(d_big));
+    for (int k = 0; k < 3; ++k) {
+        float best = 1e30f;
+        for (int rep = 0; rep < 3; ++rep) {
+            CHECK(hipEventRecord(e0, 0));
+            if (k == 0) hipLaunchKernelGGL(k_sha512_split, dim3(1), dim3(128), 0, 0, 1u, d_msg, d_off, d_len, d_dig);
+            else if (k == 1) hipLaunchKernelGGL(k_sha512_split2, dim3(1), dim3(128), 0, 0, 1u, d_msg, d_off, d_len, d_dig + 64);
+            else hipLaunchKernelGGL(k_sha512_many, dim3(1), dim3(256), 0, 0, 1u, d_msg, d_off, d_len, d_dig + 128);
+            CHECK(hipEventRecord(e1, 0));
+            CHECK(hipEventSynchronize(e1));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            best = ms < best ? ms : best;
+        }
+        printf("{\"kernel\": \"%s\", \"blocks\": %u, \"ms\": %.3f, \"ns_per_block\": %.1f}\n", names[k], nb, best,
+               best * 1e6 / nb);
+    }
+    uint8_t dg[192];
+    CHECK(hipMemcpy(dg, d_dig, 192, hipMemcpyDeviceToHost));
+    printf("{\"split_eq_many\": %s, \"split2_eq_many\": %s}\n", memcmp(dg, dg + 128, 64) ? "false" : "true",
+           memcmp(dg + 64, dg + 128, 64) ? "false" : "true");
+    return 0;
+}
