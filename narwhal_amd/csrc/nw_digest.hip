@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdlib>
 #include "nw_sha512.h"
+#include "nw_sha512_2l.h"
 #include "nw_kernels.h"
 
 namespace nw {
@@ -200,14 +201,145 @@ __global__ void __launch_bounds__(128) k_sha512_split(uint32_t n, const uint8_t*
     if (!sched && live) sha512_digest_store(out + (size_t)i * 64, st);
 }
 
+// ------------------------------------------------------------------------------------ two-lane split
+// k_sha512_split with the rounds on lane pairs (nw_sha512_2l.h: 20 instructions per round for one
+// message instead of 27): 32 messages per workgroup, lane pair (2j, 2j+1) of both waves serves
+// message j.  The schedule wave stores K_t + W_t in the even lane's column and 1 in the odd lane's
+// (the odd lane's "kw" turns its oldest value into its negation, see nw_sha512_2l.h).
+//
+// With the rounds at ~3.1 us per block the schedule wave becomes the limit if it waits for its block:
+// one HBM round trip (~1-2 us, more on a TLB miss) plus ~2.2 us of schedule arithmetic.  So the
+// block words are loaded TWO blocks ahead into a register ring (aligned full blocks; the padding
+// block(s) and unaligned messages take the synchronous sha512_load_block), and the arithmetic of
+// block b + 1 runs while block b + 3's words are in flight.
+static constexpr uint32_t SPLIT2_MSGS = 32;
+
+__device__ __forceinline__ void split2_store(const uint64_t w0[16], uint64_t (*kwb)[SPLIT_MSGS], uint32_t lane) {
+    const bool odd = lane & 1u;
+    uint64_t w[16];
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        w[t] = w0[t];
+        kwb[t][lane] = odd ? 1ull : w[t] + SHA512_K[t];
+    }
+#pragma unroll
+    for (int r = 16; r < 80; r += 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+            const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
+            const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
+            w[i] += s0 + w[(i + 9) & 15] + s1;
+            kwb[r + i][lane] = odd ? 1ull : w[i] + SHA512_K[r + i];
+        }
+    }
+}
+
+// Block k's raw dwords, loaded ahead of use when the block is a full aligned one (else nothing).
+struct RawBlock {
+    uint32_t u[32];
+    __device__ __forceinline__ void issue(const uint8_t* m, uint64_t L, uint64_t k, uint32_t nb) {
+        if (k < nb && k < L / 128 && (reinterpret_cast<uintptr_t>(m) & 3u) == 0) {
+            const uint32_t* q = reinterpret_cast<const uint32_t*>(m + k * 128);
+#pragma unroll
+            for (int j = 0; j < 32; ++j) u[j] = q[j];
+        }
+    }
+    __device__ __forceinline__ void words(const uint8_t* m, uint64_t L, uint64_t k, uint64_t w[16]) const {
+        if (k < L / 128 && (reinterpret_cast<uintptr_t>(m) & 3u) == 0) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) w[j] = be64_from_le32(u[2 * j], u[2 * j + 1]);
+        } else {
+            sha512_load_block(m, L, k, w);
+        }
+    }
+};
+
+__global__ void __launch_bounds__(128) k_sha512_split2(uint32_t n, const uint8_t* base, const uint64_t* off,
+                                                       const uint64_t* len, uint8_t* out) {
+    __shared__ uint64_t kw[2][80][SPLIT_MSGS];
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool sched = threadIdx.x >= 64;          // wave-uniform
+    const bool odd = lane & 1u;
+    const uint32_t i = blockIdx.x * SPLIT2_MSGS + (lane >> 1);
+    const bool live = i < n;
+    const uint64_t L = live ? len[i] : 0;
+    const uint8_t* m = base + (live ? off[i] : 0);
+    const uint32_t nb = live ? sha512_nblocks(L) : 0u;
+    uint32_t nbmax = nb;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, o, 64));
+    if (sched) {
+        // ring: rr[k & 1] holds block k's words from two iterations earlier
+        RawBlock rr[2];
+        uint64_t w[16];
+        if (nb > 0) {
+            sha512_load_block(m, L, 0, w);
+            rr[1].issue(m, L, 1, nb);
+            rr[0].issue(m, L, 2, nb);
+            split2_store(w, kw[0], lane);
+        }
+        __syncthreads();
+        for (uint32_t b = 0; b < nbmax; b += 2) {
+            // block b + 1 (ring slot 1), then prefetch block b + 3 into it
+            if (b + 1 < nb) {
+                rr[1].words(m, L, b + 1, w);
+                rr[1].issue(m, L, b + 3, nb);
+                split2_store(w, kw[1], lane);
+            }
+            __syncthreads();
+            if (b + 1 >= nbmax) break;
+            // block b + 2 (ring slot 0), then prefetch block b + 4
+            if (b + 2 < nb) {
+                rr[0].words(m, L, b + 2, w);
+                rr[0].issue(m, L, b + 4, nb);
+                split2_store(w, kw[0], lane);
+            }
+            __syncthreads();
+        }
+    } else {
+        uint64_t h[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[k] = SHA512_IV[(odd ? 0 : 4) + k];
+        Sha2L c;
+        c.init(odd);
+        __syncthreads();
+        for (uint32_t b = 0; b < nbmax; ++b) {
+            if (b < nb) {
+                const uint64_t (*kb)[SPLIT_MSGS] = kw[b & 1];
+                c.block(h, [&](int t) { return kb[t][lane]; });
+            }
+            __syncthreads();
+        }
+        if (live) {
+            // odd lane: a b c d = digest bytes 0..31; even lane: e f g h = bytes 32..63
+            uint4* o = reinterpret_cast<uint4*>(out + (size_t)i * 64 + (odd ? 0 : 32));
+            uint32_t d[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                d[2 * k] = bswap32((uint32_t)(h[k] >> 32));
+                d[2 * k + 1] = bswap32((uint32_t)h[k]);
+            }
+            o[0] = make_uint4(d[0], d[1], d[2], d[3]);
+            o[1] = make_uint4(d[4], d[5], d[6], d[7]);
+        }
+    }
+}
+
 hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                               uint8_t* out, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    static const bool nosplit = std::getenv("NW_SHA_NOSPLIT") != nullptr;   // A/B knob (tools/)
-    if (n <= SPLIT_MAX_N && !nosplit)
-        hipLaunchKernelGGL(k_sha512_split, dim3(blocks_for(n, SPLIT_MSGS)), dim3(128), 0, st, n, base, off, len, out);
-    else
+    static const bool nosplit = std::getenv("NW_SHA_NOSPLIT") != nullptr;   // A/B knobs (tools/)
+    static const bool split1 = std::getenv("NW_SHA_SPLIT1") != nullptr;
+    if (n <= SPLIT_MAX_N && !nosplit) {
+        if (split1)
+            hipLaunchKernelGGL(k_sha512_split, dim3(blocks_for(n, SPLIT_MSGS)), dim3(128), 0, st, n, base, off, len, out);
+        else
+            hipLaunchKernelGGL(k_sha512_split2, dim3(blocks_for(n, SPLIT2_MSGS)), dim3(128), 0, st, n, base, off, len,
+                               out);
+    } else {
         hipLaunchKernelGGL(k_sha512_many, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, base, off, len, out);
+    }
     return hipGetLastError();
 }
 

@@ -14,10 +14,13 @@ namespace nw {
 // Digits are taken from k' = k + sum_p 2^(W-1) 2^(W p) (signed radix-2^W digit p = window p of k'
 // minus 2^(W-1)), so any lane can start at any position without the serial carry chain.  The
 // output record is the one k_verify writes, for the same k_finish.
-static constexpr int VERIFY_SPLIT = 4;
-// VERIFY_SPLIT_MAX_SIGS (nw_verify_kernels.h): the split grid is then <= one wave per SIMD
-// (1,024 SIMDs x 64 lanes / VERIFY_SPLIT)
-static_assert(VERIFY_SPLIT_MAX_SIGS * VERIFY_SPLIT <= 256 * 4 * 64, "split grid larger than one wave per SIMD");
+// 8 lanes per signature: ceil(NPOS / 8) mixed additions per lane (3 at W20) + 3 shuffle levels of
+// full additions = 6 dependent point operations (~51 field products) against 6 + 2 (~62) with 4
+// lanes; 16 lanes would be 2 + 4 (~54).
+static constexpr int VERIFY_SPLIT = 8;
+// VERIFY_SPLIT_MAX_SIGS (nw_verify_kernels.h): the split grid is then <= two waves per SIMD
+// (1,024 SIMDs x 64 lanes x 2 / VERIFY_SPLIT)
+static_assert(VERIFY_SPLIT_MAX_SIGS * VERIFY_SPLIT <= 2 * 256 * 4 * 64, "split grid larger than two waves per SIMD");
 
 // k + sum_{p < comb_pos(W)} 2^(W-1) 2^(W p) for k < 2^253 (< 2^(W comb_pos(W)) for every window).
 template <int W>
@@ -83,34 +86,53 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
     for (int q = 0; q < p0 && q < PB; ++q) shift_window<WB>(sp);
     for (int q = PB; q < p0; ++q) shift_window<WA>(hp);
     const uint32_t* atab = a.key_tab + (size_t)slot * comb_words(WA);
-    ge_p3 P;
-#pragma unroll 1
+    // all K digits first (cheap shifts), so each table entry's 128-B gather can be issued one
+    // position ahead, under the previous mixed addition (the entries are cold in L2: a lone
+    // signature's chain would otherwise wait a full memory round trip per position)
+    int dig[K];
+#pragma unroll
     for (int st = 0; st < K; ++st) {
+        const bool base = p0 + st < PB;
+        dig[st] = base ? low_digit<WB>(sp) : low_digit<WA>(hp);
+        if (base) shift_window<WB>(sp);
+        else shift_window<WA>(hp);
+    }
+    auto entry = [&](int st) -> const uint4* {
         const int pos = p0 + st;
-        const bool base = pos < PB;
-        const int db = low_digit<WB>(sp), dk = low_digit<WA>(hp);
-        const int d = base ? db : dk;
-        const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+        const uint32_t ad = (uint32_t)(dig[st] < 0 ? -dig[st] : dig[st]);
         // past the last position: entry 0 of base position 0 (the identity), a no-op addition
         const uint32_t* e = pos >= NPOS ? a.btab
-                            : base      ? a.btab + ((size_t)pos * comb_ent(WB) + ad) * PRECOMP_WORDS
+                            : pos < PB  ? a.btab + ((size_t)pos * comb_ent(WB) + ad) * PRECOMP_WORDS
                                         : atab + ((size_t)(pos - PB) * comb_ent(WA) + ad) * PRECOMP_WORDS;
-        const uint4* q = reinterpret_cast<const uint4*>(e);
+        return reinterpret_cast<const uint4*>(e);
+    };
+    uint4 nx[8];
+    {
+        const uint4* q = entry(0);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) nx[k] = q[k];
+    }
+    ge_p3 P;
+#pragma unroll
+    for (int st = 0; st < K; ++st) {
+        const int pos = p0 + st;
         uint32_t w[32];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const uint4 v = q[k];
-            w[4 * k] = v.x;
-            w[4 * k + 1] = v.y;
-            w[4 * k + 2] = v.z;
-            w[4 * k + 3] = v.w;
+            w[4 * k] = nx[k].x;
+            w[4 * k + 1] = nx[k].y;
+            w[4 * k + 2] = nx[k].z;
+            w[4 * k + 3] = nx[k].w;
         }
-        const bool neg = pos < NPOS && (base ? d < 0 : d > 0);
+        if (st + 1 < K) {
+            const uint4* q = entry(st + 1);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) nx[k] = q[k];
+        }
+        const bool neg = pos < NPOS && (pos < PB ? dig[st] < 0 : dig[st] > 0);
         const ge_precomp ent = ge_precomp_cneg(ge_precomp_from_words(w), neg);
         if (st == 0) P = ge_from_precomp(ent);
         else P = ge_madd(P, ent);
-        if (base) shift_window<WB>(sp);
-        else shift_window<WA>(hp);
     }
 #pragma unroll
     for (int off = 1; off < VERIFY_SPLIT; off <<= 1) {
