@@ -128,7 +128,7 @@ struct Workspace {
     DevBuf w_sig, w_signer, w_keys, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len, w_flags,
         w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_ok, w_misc, w_out, w_pbuf, w_pre, w_counts,
         w_cursor, w_perm, w_io, w_var, w_status, w_msm_ent, w_msm_dig, w_msm_zs, w_msm_meta, w_msm_bkt, w_msm_part,
-        w_msm_wpart, w_pslow, w_cert_state;
+        w_msm_wpart, w_pslow, w_cert_state, w_exact;
     HostBuf h_io, h_meta;
 
     // Grow a buffer; a buffer that may still be read by a pending call is only freed after it.
@@ -145,7 +145,7 @@ struct Workspace {
                           &w_msg_len, &w_flags, &w_slow_count, &w_slow_list, &w_slow_slot, &w_slow_buf, &w_cert_ok,
                           &w_ok, &w_misc, &w_out, &w_pbuf, &w_pre, &w_counts, &w_cursor, &w_perm, &w_io, &w_var,
                           &w_status, &w_msm_ent, &w_msm_dig, &w_msm_zs, &w_msm_meta, &w_msm_bkt, &w_msm_part,
-                          &w_msm_wpart, &w_pslow, &w_cert_state})
+                          &w_msm_wpart, &w_pslow, &w_cert_state, &w_exact})
             b->release();
         h_io.release();
         h_meta.release();
@@ -522,6 +522,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
         NW_TRY(ws->ensure(ws->w_slow_buf, nsigs * (size_t)SLOW_WORDS * 4 + 4), "ws slow_buf");
         NW_TRY(ws->ensure(ws->w_pslow, nsigs * (size_t)160 + 16), "ws pslow");
         NW_TRY(ws->ensure(ws->w_cert_state, ncerts * 4 + 16), "ws cert_state");
+        NW_TRY(ws->ensure(ws->w_exact, ncerts * 4 + 16), "ws exact list");
     }
     NW_TRY(ws->ensure(ws->w_pbuf, nsigs * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
     NW_TRY(ws->ensure(ws->w_pre, nsigs * 40 + 16), "ws pre");
@@ -622,7 +623,9 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     fp.cert_ok = d_cert_ok;
     fp.accepted_stake = d_stake_out;
     fp.sig_ok = d_sig_ok;
-    NW_TRY(launch_finalize(fp, st), "k_cert_finalize");
+    fp.exact_count = slow_count + 1;   // word 1 of the zeroed slow-path counter block
+    fp.exact_list = ws->w_exact.as<uint32_t>();
+    NW_TRY(launch_finalize(fp, st), "k_cert_finalize / k_cert_exact");
     return NW_OK;
 }
 

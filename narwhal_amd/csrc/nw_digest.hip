@@ -203,50 +203,38 @@ __global__ void __launch_bounds__(128) k_sha512_split(uint32_t n, const uint8_t*
 
 // ------------------------------------------------------------------------------------ two-lane split
 // k_sha512_split with the rounds on lane pairs (nw_sha512_2l.h: 20 instructions per round for one
-// message instead of 27): 32 messages per workgroup, lane pair (2j, 2j+1) of both waves serves
-// message j.  The schedule wave stores K_t + W_t in the even lane's column and 1 in the odd lane's
-// (the odd lane's "kw" turns its oldest value into its negation, see nw_sha512_2l.h).
+// message instead of 27): 32 messages per workgroup; lane pair (2j, 2j+1) of the round wave serves
+// message j.
 //
-// With the rounds at ~3.1 us per block the schedule wave becomes the limit if it waits for its block:
-// one HBM round trip (~1-2 us, more on a TLB miss) plus ~2.2 us of schedule arithmetic.  So the
-// block words are loaded TWO blocks ahead into a register ring (aligned full blocks; the padding
-// block(s) and unaligned messages take the synchronous sha512_load_block), and the arithmetic of
-// block b + 1 runs while block b + 3's words are in flight.
+// At ~3.1 us per block for the rounds, one schedule wave (~3 us of arithmetic per block plus its
+// block loads) would set the pace, so TWO schedule waves alternate blocks, each doing half a block's
+// schedule per period (one period = the rounds of one block, closed by a barrier):
+//   wave A (even blocks), period p:  p even: rows 0..47 of block p + 2;   p odd: rows 48..79 of block p + 1
+//   wave B (odd blocks),  period p:  p even: rows 48..79 of block p + 1;  p odd: rows 0..47 of block p + 2
+// Block k lives in buffer k % 3 (written in periods k-2 and k-1, read in period k).  A schedule
+// wave keeps its 16-word ring in registers between the halves, and loads its next block's words
+// one own-block (two periods) ahead.  K_t + W_t is stored once per message (column j); the odd
+// lanes of the round wave read a constant column of 1s (their "kw" turns the oldest value into
+// its negation, see nw_sha512_2l.h), written once at the start.
 static constexpr uint32_t SPLIT2_MSGS = 32;
-
-__device__ __forceinline__ void split2_store(const uint64_t w0[16], uint64_t (*kwb)[SPLIT_MSGS], uint32_t lane) {
-    const bool odd = lane & 1u;
-    uint64_t w[16];
-#pragma unroll
-    for (int t = 0; t < 16; ++t) {
-        w[t] = w0[t];
-        kwb[t][lane] = odd ? 1ull : w[t] + SHA512_K[t];
-    }
-#pragma unroll
-    for (int r = 16; r < 80; r += 16) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-            const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
-            const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
-            w[i] += s0 + w[(i + 9) & 15] + s1;
-            kwb[r + i][lane] = odd ? 1ull : w[i] + SHA512_K[r + i];
-        }
-    }
-}
+static constexpr uint32_t SPLIT2_COLS = SPLIT2_MSGS + 1;   // + the column of 1s
+static constexpr int SPLIT2_HALF = 48;                      // rows of the first half (16 loaded + 32 computed)
 
 // Block k's raw dwords, loaded ahead of use when the block is a full aligned one (else nothing).
 struct RawBlock {
     uint32_t u[32];
+    __device__ __forceinline__ static bool fast(const uint8_t* m, uint64_t L, uint64_t k) {
+        return k < L / 128 && (reinterpret_cast<uintptr_t>(m) & 3u) == 0;
+    }
     __device__ __forceinline__ void issue(const uint8_t* m, uint64_t L, uint64_t k, uint32_t nb) {
-        if (k < nb && k < L / 128 && (reinterpret_cast<uintptr_t>(m) & 3u) == 0) {
+        if (k < nb && fast(m, L, k)) {
             const uint32_t* q = reinterpret_cast<const uint32_t*>(m + k * 128);
 #pragma unroll
             for (int j = 0; j < 32; ++j) u[j] = q[j];
         }
     }
     __device__ __forceinline__ void words(const uint8_t* m, uint64_t L, uint64_t k, uint64_t w[16]) const {
-        if (k < L / 128 && (reinterpret_cast<uintptr_t>(m) & 3u) == 0) {
+        if (fast(m, L, k)) {
 #pragma unroll
             for (int j = 0; j < 16; ++j) w[j] = be64_from_le32(u[2 * j], u[2 * j + 1]);
         } else {
@@ -255,59 +243,55 @@ struct RawBlock {
     }
 };
 
-__global__ void __launch_bounds__(128) k_sha512_split2(uint32_t n, const uint8_t* base, const uint64_t* off,
+// Schedule rows [R0, R1) of the block whose first 16 words are in w (the ring advances in place:
+// after row t >= 16 is produced, w[t & 15] holds W_t).
+template <int R0, int R1>
+__device__ __forceinline__ void split2_rows(uint64_t w[16], uint64_t (*kwb)[SPLIT2_COLS], uint32_t col) {
+#pragma unroll
+    for (int t = R0; t < R1; ++t) {
+        if (t >= 16) {
+            const int i = t & 15;
+            const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+            const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
+            const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
+            w[i] += s0 + w[(i + 9) & 15] + s1;
+        }
+        kwb[t][col] = w[t & 15] + SHA512_K[t];
+    }
+}
+
+// PROBE (tools/sha_lone.hip only): 1 = schedule waves skip their arithmetic, 2 = the round wave
+// skips its rounds (both keep every barrier), to time each side alone.
+template <int PROBE = 0>
+__global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t* base, const uint64_t* off,
                                                        const uint64_t* len, uint8_t* out) {
-    __shared__ uint64_t kw[2][80][SPLIT_MSGS];
+    __shared__ uint64_t kw[3][80][SPLIT2_COLS];   // 63,360 B: two workgroups per CU
+    const uint32_t wave = threadIdx.x >> 6;         // 0: rounds, 1: schedule A, 2: schedule B
     const uint32_t lane = threadIdx.x & 63u;
-    const bool sched = threadIdx.x >= 64;          // wave-uniform
     const bool odd = lane & 1u;
-    const uint32_t i = blockIdx.x * SPLIT2_MSGS + (lane >> 1);
-    const bool live = i < n;
+    // rounds: lane pair (2j, 2j+1) -> message j; schedule: lane j < 32 -> message j
+    const uint32_t j = wave == 0 ? lane >> 1 : lane;
+    const uint32_t i = blockIdx.x * SPLIT2_MSGS + j;
+    const bool live = j < SPLIT2_MSGS && i < n;
     const uint64_t L = live ? len[i] : 0;
     const uint8_t* m = base + (live ? off[i] : 0);
     const uint32_t nb = live ? sha512_nblocks(L) : 0u;
     uint32_t nbmax = nb;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, o, 64));
-    if (sched) {
-        // ring: rr[k & 1] holds block k's words from two iterations earlier
-        RawBlock rr[2];
-        uint64_t w[16];
-        if (nb > 0) {
-            sha512_load_block(m, L, 0, w);
-            rr[1].issue(m, L, 1, nb);
-            rr[0].issue(m, L, 2, nb);
-            split2_store(w, kw[0], lane);
-        }
-        __syncthreads();
-        for (uint32_t b = 0; b < nbmax; b += 2) {
-            // block b + 1 (ring slot 1), then prefetch block b + 3 into it
-            if (b + 1 < nb) {
-                rr[1].words(m, L, b + 1, w);
-                rr[1].issue(m, L, b + 3, nb);
-                split2_store(w, kw[1], lane);
-            }
-            __syncthreads();
-            if (b + 1 >= nbmax) break;
-            // block b + 2 (ring slot 0), then prefetch block b + 4
-            if (b + 2 < nb) {
-                rr[0].words(m, L, b + 2, w);
-                rr[0].issue(m, L, b + 4, nb);
-                split2_store(w, kw[0], lane);
-            }
-            __syncthreads();
-        }
-    } else {
+    if (wave == 0) {
+        for (uint32_t t = lane; t < 3 * 80; t += 64) kw[t / 80][t % 80][SPLIT2_MSGS] = 1ull;
         uint64_t h[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) h[k] = SHA512_IV[(odd ? 0 : 4) + k];
         Sha2L c;
         c.init(odd);
+        const uint32_t col = odd ? SPLIT2_MSGS : j;
         __syncthreads();
         for (uint32_t b = 0; b < nbmax; ++b) {
-            if (b < nb) {
-                const uint64_t (*kb)[SPLIT_MSGS] = kw[b & 1];
-                c.block(h, [&](int t) { return kb[t][lane]; });
+            if (b < nb && PROBE != 2) {
+                const uint64_t (*kb)[SPLIT2_COLS] = kw[b % 3];
+                c.block(h, [&](int t) { return kb[t][col]; });
             }
             __syncthreads();
         }
@@ -323,6 +307,35 @@ __global__ void __launch_bounds__(128) k_sha512_split2(uint32_t n, const uint8_t
             o[0] = make_uint4(d[0], d[1], d[2], d[3]);
             o[1] = make_uint4(d[4], d[5], d[6], d[7]);
         }
+        return;
+    }
+    // schedule waves: A (wave 1) owns the even blocks, B (wave 2) the odd ones
+    const uint32_t par = wave - 1;
+    RawBlock rb;
+    uint64_t w[16];
+    const uint32_t k0 = par;                       // first own block
+    if (k0 < nb && PROBE != 1) {
+        sha512_load_block(m, L, k0, w);            // synchronous: nothing was issued yet
+        rb.issue(m, L, k0 + 2, nb);
+        split2_rows<0, SPLIT2_HALF>(w, kw[k0 % 3], j);
+        if (par == 0) split2_rows<SPLIT2_HALF, 80>(w, kw[k0 % 3], j);   // block 0 complete before period 0
+    }
+    __syncthreads();
+    for (uint32_t p = 0; p < nbmax; ++p) {
+        if ((p & 1u) == par) {
+            // first half of own block p + 2
+            const uint32_t k = p + 2;
+            if (k < nb && PROBE != 1) {
+                rb.words(m, L, k, w);
+                rb.issue(m, L, k + 2, nb);
+                split2_rows<0, SPLIT2_HALF>(w, kw[k % 3], j);
+            }
+        } else {
+            // second half of own block p + 1
+            const uint32_t k = p + 1;
+            if (k < nb && PROBE != 1) split2_rows<SPLIT2_HALF, 80>(w, kw[k % 3], j);
+        }
+        __syncthreads();
     }
 }
 
@@ -335,7 +348,7 @@ hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* o
         if (split1)
             hipLaunchKernelGGL(k_sha512_split, dim3(blocks_for(n, SPLIT_MSGS)), dim3(128), 0, st, n, base, off, len, out);
         else
-            hipLaunchKernelGGL(k_sha512_split2, dim3(blocks_for(n, SPLIT2_MSGS)), dim3(128), 0, st, n, base, off, len,
+            hipLaunchKernelGGL(k_sha512_split2<0>, dim3(blocks_for(n, SPLIT2_MSGS)), dim3(192), 0, st, n, base, off, len,
                                out);
     } else {
         hipLaunchKernelGGL(k_sha512_many, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, base, off, len, out);

@@ -16,9 +16,8 @@ static constexpr uint32_t NW_F_TCOEF_SHIFT = 8;   // 3 bits of per-signature tor
 // z_i mod 8.
 static constexpr int SLOW_WORDS = 44;
 static constexpr int SLOW_KIND = 40;              // word: SK_*
-static constexpr int SLOW_Z8 = 41;                // word: z_i mod 8 (SK_SMALL)
 static constexpr uint32_t SK_SKIP = 0;            // certificate already rejected: no point computed
-static constexpr uint32_t SK_SMALL = 1;           // D_i of small order (or z_i = 0): z_i D_i = (z_i mod 8) D_i
+static constexpr uint32_t SK_SMALL = 1;           // D_i of small order (or z_i = 0): record = (z_i mod 8) D_i
 static constexpr uint32_t SK_BIG = 2;             // D_i has a prime-order component and z_i != 0
 static constexpr uint32_t SK_MUL = 3;             // SK_BIG whose z_i D_i was computed (record holds z_i D_i)
 // Per-certificate exact-path state word: the number of SK_BIG entries, and a flag set as soon as
@@ -83,6 +82,8 @@ struct FinalizeParams {
     uint8_t* cert_ok;              // [ncerts] (may be null)
     uint64_t* accepted_stake;      // [ncerts] (may be null)
     uint8_t* sig_ok;               // [nsigs] strict verdict bytes (may be null; k_flags_to_ok fused)
+    uint32_t* exact_count;         // device counter (zeroed by the preamble) of ...
+    uint32_t* exact_list;          // [ncerts] ... certificates whose verdict needs the exact sum (k_cert_exact)
 };
 
 hipError_t launch_verify(const VerifyParams& p, int msgmode, int key_window, hipStream_t st);

@@ -172,13 +172,11 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
 // exact remaining batch sum (usually empty) must be the identity.  One 64-lane wave per
 // certificate: lanes stride over the votes (coalesced flag reads), wave reductions combine them;
 // the exact sum over slow-path terms (failing certificates only) is a lane-strided sum + shuffle tree.
-// Occupancy bound: the common path (flag reduction, stake sum) needs few registers, the rare exact
-// sum over failing votes (ge_add chain) many; bounding the kernel to 8 waves per SIMD (64 VGPRs)
-// lets the rare path spill instead of capping every certificate's wave at 3 per SIMD.
-#ifndef NW_FINALIZE_WAVES
-#define NW_FINALIZE_WAVES 8
-#endif
-__global__ void __launch_bounds__(256, NW_FINALIZE_WAVES) k_cert_finalize(FinalizeParams a) {
+// One wave per certificate: flag reduction, stake sum, and the verdict whenever the flags decide it
+// (parse / decode failure, all votes matching, one term with a prime-order component).  The rest
+// (two or more slow-path terms) is appended to the exact list for k_cert_exact, which has the
+// registers for the point sum: this kernel stays at a handful of VGPRs and never spills.
+__global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if (a.sig_ok) {   // strict verdict bytes of every signature (the flags are final here)
@@ -209,6 +207,8 @@ __global__ void __launch_bounds__(256, NW_FINALIZE_WAVES) k_cert_finalize(Finali
         tsum += __shfl_xor(tsum, off, 64);
         stake += __shfl_xor(stake, off, 64);
     }
+    if (lane != 0) return;
+    if (a.accepted_stake) a.accepted_stake[c] = stake;
     bool ok;
     if (bad) {
         ok = false;
@@ -217,37 +217,61 @@ __global__ void __launch_bounds__(256, NW_FINALIZE_WAVES) k_cert_finalize(Finali
     } else if ((a.cert_state[c] & CS_BIG_MASK) == 1u) {
         ok = false;   // one term with a prime-order component: the sum cannot be the identity (k_slow_prep)
     } else {
-        // exact sum of the slow-path terms: z_i D_i computed by k_slow_mul (SK_MUL), or (z_i mod 8) D_i
-        // for small-order D_i (SK_SMALL, at most 3 doublings + 3 additions); lanes stride over the
-        // votes, then a shuffle tree
+        a.exact_list[atomicAdd(a.exact_count, 1u)] = c;   // k_cert_exact writes the verdict
+        return;
+    }
+    if (a.cert_ok) a.cert_ok[c] = ok ? 1 : 0;
+}
+
+// Exact sum of a listed certificate (one wave each, grid-stride over the list): every slow vote's
+// record holds its term z_i D_i (k_slow_mul for prime-order components, k_slow_prep's (z_i mod 8) D_i
+// for small-order ones), the torsion coefficients of the matching votes add (sum mod 8) T8.  Lanes
+// sum their votes' terms, the lanes that hold a term are compacted through LDS, and a shuffle tree
+// of ceil(log2(count)) levels adds them: the serial chain is a few point additions, not six levels
+// plus per-term multiples.
+static constexpr uint32_t EXACT_MAX_BLOCKS = 1024;
+__global__ void __launch_bounds__(64) k_cert_exact(FinalizeParams a) {
+    __shared__ uint32_t part[64][40];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t cnt = *a.exact_count;
+    for (uint32_t e = blockIdx.x; e < cnt; e += gridDim.x) {
+        const uint32_t c = a.exact_list[e];
+        const uint32_t first = a.cert_first[c], nv = a.cert_n[c];   // in range: bad ranges never get listed
         ge_p3 acc = ge_to_vgpr(ge_identity());
+        bool has = false;
+        uint32_t tsum = 0;
         for (uint32_t v = lane; v < nv; v += 64) {
-            if (a.flags[first + v] & NW_F_SLOW) {
-                const uint32_t* rec = a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS;
-                const ge_p3 Q = load_p3(rec);
-                if (rec[SLOW_KIND] == SK_MUL) {
-                    acc = ge_add(acc, ge_to_cached(Q));
-                } else {
-                    const uint32_t z8 = rec[SLOW_Z8];
-                    const ge_cached qc = ge_to_cached(Q);
-                    ge_p3 m = ge_to_vgpr(ge_identity());
-                    for (int bit = 2; bit >= 0; --bit) {
-                        m = ge_dbl(m);
-                        if ((z8 >> bit) & 1u) m = ge_add(m, qc);
-                    }
-                    acc = ge_add(acc, ge_to_cached(m));
-                }
+            const uint32_t f = a.flags[first + v];
+            tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
+            if (f & NW_F_SLOW) {
+                const ge_p3 q = load_p3(a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS);
+                acc = has ? ge_add(acc, ge_to_cached(q)) : q;
+                has = true;
             }
         }
 #pragma unroll
-        for (unsigned off = 32; off > 0; off >>= 1) acc = ge_add(acc, ge_to_cached(ge_shfl_down(acc, off)));
-        const ge_cached t8c = ge_to_cached(ge_t8());
-        for (uint32_t k = 0; k < (tsum & 7u); ++k) acc = ge_add(acc, t8c);
-        ok = ge_is_identity(acc);
+        for (int off = 32; off > 0; off >>= 1) tsum += __shfl_xor(tsum, off, 64);
+        const uint32_t tk = tsum & 7u;
+        if (lane == 63 && tk != 0) {   // lane 63 adds (tk) T8 to its partial (binary: T8, 2 T8, 4 T8)
+            const ge_p3 t1 = ge_t8(), t2 = ge_dbl(t1), t4 = ge_dbl(t2);
+            ge_p3 t = ge_select(ge_identity(), t1, (tk & 1u) != 0);
+            t = ge_add(t, ge_to_cached(ge_select(ge_identity(), t2, (tk & 2u) != 0)));
+            t = ge_add(t, ge_to_cached(ge_select(ge_identity(), t4, (tk & 4u) != 0)));
+            acc = has ? ge_add(acc, ge_to_cached(t)) : t;
+            has = true;
+        }
+        const uint64_t mask = __ballot(has);
+        const uint32_t k = (uint32_t)__popcll(mask);
+        if (has) store_p3(part[__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))], acc);
+        __syncthreads();
+        acc = lane < k ? load_p3(part[lane]) : ge_identity();
+        __syncthreads();   // part is rewritten by the next listed certificate
+        for (uint32_t off = 1; off < k; off <<= 1) {   // k is wave-uniform
+            const ge_p3 o = ge_shfl_down(acc, off);
+            acc = ge_select(acc, ge_add(acc, ge_to_cached(o)), lane + off < k);
+        }
+        if (lane == 0 && a.cert_ok) a.cert_ok[c] = ge_is_identity(acc) ? 1 : 0;
     }
-    if (lane != 0) return;
-    if (a.cert_ok) a.cert_ok[c] = ok ? 1 : 0;
-    if (a.accepted_stake) a.accepted_stake[c] = stake;
 }
 
 // Device-side input check of nw_verify_certs_dev: every vote range inside [0, nsigs) and every
@@ -269,7 +293,7 @@ __global__ void __launch_bounds__(256) k_validate_certs(uint32_t ncerts, uint32_
 // MI355X, dominated by dispatch, not work.
 //   k_prep_certs:   sig_cert = 0 (votes outside every certificate map to certificate 0), the slot
 //                   counts, the slow-path counter and the status word = 0.
-//   k_expand_count: block b expands certificates [256 b, 256 b + 256) into sig_cert and, for
+//   k_expand_count: block b expands certificates [4 b, 4 b + 4) into sig_cert and, for
 //                   signature tile b (GROUP_TILE signatures), histograms the signer slots (LDS, one
 //                   global add per slot) and/or checks them; every check ORs NW_ERR_ARG into status.
 __global__ void __launch_bounds__(256) k_prep_certs(uint32_t nsigs, uint32_t nkeys, uint32_t* sig_cert, uint32_t* counts,
@@ -286,18 +310,21 @@ __global__ void __launch_bounds__(256) k_prep_certs(uint32_t nsigs, uint32_t nke
     if (status && t == 0) *status = 0u;
 }
 
+static constexpr uint32_t EXPAND_CERTS_PER_BLOCK = 4;   // one wave each
 __global__ void __launch_bounds__(256) k_expand_count(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys,
                                                       const uint32_t* cert_first, const uint32_t* cert_n,
                                                       const uint32_t* signer, uint32_t* sig_cert, uint32_t* counts,
                                                       uint32_t* status) {
     extern __shared__ uint32_t hist[];
-    const uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+    // one wave per certificate: its lanes write the vote -> certificate entries side by side (a
+    // thread per certificate would store 667 / 6,667 entries serially at C3 / C4)
+    const uint32_t c = blockIdx.x * EXPAND_CERTS_PER_BLOCK + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
     bool bad = false;
     if (c < ncerts) {
         const uint32_t f = cert_first[c], n = cert_n[c];
-        bad = (uint64_t)f + n > nsigs;
-        const uint32_t end = bad ? nsigs : f + n;   // clamped: k_cert_finalize rejects it anyway
-        for (uint32_t v = f; v < end; ++v) sig_cert[v] = c;
+        bad = lane == 0 && (uint64_t)f + n > nsigs;
+        const uint32_t end = (uint64_t)f + n > nsigs ? nsigs : f + n;   // clamped: k_cert_finalize rejects it
+        for (uint32_t v = f + lane; v < end; v += 64) sig_cert[v] = c;
     }
     const uint32_t t0 = blockIdx.x * GROUP_TILE;
     if ((counts || status) && t0 < nsigs) {
@@ -429,6 +456,10 @@ hipError_t launch_finish(const VerifyParams& p, hipStream_t st) {
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
     if (p.ncerts == 0) return hipSuccess;
     hipLaunchKernelGGL(k_cert_finalize, dim3(blocks_for((uint64_t)p.ncerts * 64, 256)), dim3(256), 0, st, p);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // the exact list's length is on the device: a capped grid that exits at once when it is empty
+    hipLaunchKernelGGL(k_cert_exact, dim3(std::min<uint32_t>(p.ncerts, EXACT_MAX_BLOCKS)), dim3(64), 0, st, p);
     return hipGetLastError();
 }
 
@@ -439,7 +470,7 @@ hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, c
     hipLaunchKernelGGL(k_prep_certs, dim3(prep_blocks), dim3(256), 0, st, nsigs, nkeys, sig_cert, counts, zero4, status,
                        ncerts, cert_state);
     const bool tiles = (counts || status) && nsigs > 0;
-    const uint32_t nb = std::max<uint32_t>(blocks_for(ncerts, 256), tiles ? blocks_for(nsigs, GROUP_TILE) : 0u);
+    const uint32_t nb = std::max<uint32_t>(blocks_for(ncerts, EXPAND_CERTS_PER_BLOCK), tiles ? blocks_for(nsigs, GROUP_TILE) : 0u);
     if (nb == 0) return hipGetLastError();
     const size_t lds = counts && nkeys <= GROUP_LDS_KEYS ? (size_t)nkeys * 4 : 0;
     hipLaunchKernelGGL(k_expand_count, dim3(nb), dim3(256), lds, st, ncerts, nsigs, nkeys, first, nv, signer, sig_cert,

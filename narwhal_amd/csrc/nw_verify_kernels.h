@@ -159,11 +159,20 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
         uint32_t z4[4];
         coeff_z(a, i, cert, z4);
         const bool zzero = (z4[0] | z4[1] | z4[2] | z4[3]) == 0;
-        const bool small = ge_is_identity(ge_dbl(ge_dbl(ge_dbl(D))));
+        const ge_p3 D2 = ge_dbl(D), D4 = ge_dbl(D2);
+        const bool small = ge_is_identity(ge_dbl(D4));
         const uint32_t kind = (small || zzero) ? SK_SMALL : SK_BIG;
-        if (kind == SK_BIG) atomicAdd(&a.cert_state[cert], 1u);
-        store_p3(rec, D);
-        rec[SLOW_Z8] = z4[0] & 7u;
+        if (kind == SK_BIG) {
+            atomicAdd(&a.cert_state[cert], 1u);
+            store_p3(rec, D);
+        } else {
+            // the term itself: z_i D_i = (z_i mod 8) D_i from D, 2D, 4D (k_cert_exact only adds records)
+            const uint32_t z8 = zzero ? 0u : (z4[0] & 7u);
+            ge_p3 t = ge_select(ge_identity(), D, (z8 & 1u) != 0);
+            t = ge_add(t, ge_to_cached(ge_select(ge_identity(), D2, (z8 & 2u) != 0)));
+            t = ge_add(t, ge_to_cached(ge_select(ge_identity(), D4, (z8 & 4u) != 0)));
+            store_p3(rec, t);
+        }
         rec[SLOW_KIND] = kind;
     }
 }

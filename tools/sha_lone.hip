@@ -199,7 +199,7 @@ int main(int argc, char** argv) {
     CHECK(hipMalloc(&d_msg, L + 64));
     CHECK(hipMalloc(&d_off, 8));
     CHECK(hipMalloc(&d_len, 8));
-    CHECK(hipMalloc(&d_dig, 64 * 3));
+    CHECK(hipMalloc(&d_dig, 64 * 4));
     CHECK(hipMemset(d_msg, 0x5A, L));
     const uint64_t zero = 0;
     CHECK(hipMemcpy(d_off, &zero, 8, hipMemcpyHostToDevice));
@@ -207,7 +207,8 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    const char* names[3] = {"k_sha512_split", "k_sha512_split2", "k_sha512_many"};
+    const char* names[5] = {"k_sha512_split", "k_sha512_split2", "k_sha512_many", "split2_rounds_only",
+                            "split2_schedule_only"};
     // the same message at the far end of a 4 GiB buffer (the bench's 10,000 worker batches are one
     // 5 GB tensor): fresh pages / TLB reach
     uint8_t* d_big;
@@ -223,7 +224,7 @@ int main(int argc, char** argv) {
         for (int rep = 0; rep < 3; ++rep) {
             CHECK(hipEventRecord(e0, 0));
             if (k == 0) hipLaunchKernelGGL(k_sha512_split, dim3(1), dim3(128), 0, 0, 1u, d_big, d_off_far, d_len, d_dig);
-            else hipLaunchKernelGGL(k_sha512_split2, dim3(1), dim3(128), 0, 0, 1u, d_big, d_off_far, d_len, d_dig + 64);
+            else hipLaunchKernelGGL(k_sha512_split2<0>, dim3(1), dim3(192), 0, 0, 1u, d_big, d_off_far, d_len, d_dig + 64);
             CHECK(hipEventRecord(e1, 0));
             CHECK(hipEventSynchronize(e1));
             float ms;
@@ -234,21 +235,24 @@ int main(int argc, char** argv) {
                "\"ns_per_block\": %.1f}\n", names[k], nb, best, best * 1e6 / nb);
     }
     CHECK(hipFree(d_big));
-    for (int k = 0; k < 3; ++k) {
-        float best = 1e30f;
-        for (int rep = 0; rep < 3; ++rep) {
+    for (int k = 0; k < 5; ++k) {
+        float best = 1e30f, worst = 0.f;
+        for (int rep = 0; rep < 5; ++rep) {
             CHECK(hipEventRecord(e0, 0));
             if (k == 0) hipLaunchKernelGGL(k_sha512_split, dim3(1), dim3(128), 0, 0, 1u, d_msg, d_off, d_len, d_dig);
-            else if (k == 1) hipLaunchKernelGGL(k_sha512_split2, dim3(1), dim3(128), 0, 0, 1u, d_msg, d_off, d_len, d_dig + 64);
-            else hipLaunchKernelGGL(k_sha512_many, dim3(1), dim3(256), 0, 0, 1u, d_msg, d_off, d_len, d_dig + 128);
+            else if (k == 1) hipLaunchKernelGGL(k_sha512_split2<0>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_dig + 64);
+            else if (k == 2) hipLaunchKernelGGL(k_sha512_many, dim3(1), dim3(256), 0, 0, 1u, d_msg, d_off, d_len, d_dig + 128);
+            else if (k == 3) hipLaunchKernelGGL(k_sha512_split2<1>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_dig + 192);
+            else hipLaunchKernelGGL(k_sha512_split2<2>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_dig + 192);
             CHECK(hipEventRecord(e1, 0));
             CHECK(hipEventSynchronize(e1));
             float ms;
             CHECK(hipEventElapsedTime(&ms, e0, e1));
             best = ms < best ? ms : best;
+            worst = ms > worst ? ms : worst;
         }
-        printf("{\"kernel\": \"%s\", \"blocks\": %u, \"ms\": %.3f, \"ns_per_block\": %.1f}\n", names[k], nb, best,
-               best * 1e6 / nb);
+        printf("{\"kernel\": \"%s\", \"blocks\": %u, \"ms\": %.3f, \"ns_per_block\": %.1f, \"worst_ns_per_block\": %.1f}\n",
+               names[k], nb, best, best * 1e6 / nb, worst * 1e6 / nb);
     }
     uint8_t dg[192];
     CHECK(hipMemcpy(dg, d_dig, 192, hipMemcpyDeviceToHost));
