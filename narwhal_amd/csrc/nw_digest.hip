@@ -244,24 +244,31 @@ struct RawBlock {
 };
 
 // Schedule rows [R0, R1) of the block whose first 16 words are in w (the ring advances in place:
-// after row t >= 16 is produced, w[t & 15] holds W_t).
+// after row t >= 16 is produced, w[t & 15] holds W_t).  Rows 16.. run as 16-row groups in a rolled
+// loop: the kernel's code (three waves' worth of it) stays well inside the instruction cache.
 template <int R0, int R1>
 __device__ __forceinline__ void split2_rows(uint64_t w[16], uint64_t (*kwb)[SPLIT2_COLS], uint32_t col) {
+    static_assert(R0 % 16 == 0 && R1 % 16 == 0, "16-row groups");
+    if (R0 == 0) {
 #pragma unroll
-    for (int t = R0; t < R1; ++t) {
-        if (t >= 16) {
-            const int i = t & 15;
+        for (int t = 0; t < 16; ++t) kwb[t][col] = w[t] + SHA512_K[t];
+    }
+#pragma nounroll
+    for (int g = (R0 < 16 ? 16 : R0); g < R1; g += 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
             const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
             const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
             const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
             w[i] += s0 + w[(i + 9) & 15] + s1;
+            kwb[g + i][col] = w[i] + SHA512_K[g + i];
         }
-        kwb[t][col] = w[t & 15] + SHA512_K[t];
     }
 }
 
 // PROBE (tools/sha_lone.hip only): 1 = schedule waves skip their arithmetic, 2 = the round wave
-// skips its rounds (both keep every barrier), to time each side alone.
+// skips its rounds (both keep every barrier), to time each side alone; 3 = the round wave writes
+// its shader cycles and 100 MHz ticks instead of the digest.
 template <int PROBE = 0>
 __global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t* base, const uint64_t* off,
                                                        const uint64_t* len, uint8_t* out) {
@@ -280,6 +287,9 @@ __global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, o, 64));
     if (wave == 0) {
+        // the round wave is the chain's critical path: when it shares a SIMD with a schedule wave, the
+        // arbiter should pick it first
+        __builtin_amdgcn_s_setprio(3);
         for (uint32_t t = lane; t < 3 * 80; t += 64) kw[t / 80][t % 80][SPLIT2_MSGS] = 1ull;
         uint64_t h[4];
 #pragma unroll
@@ -288,12 +298,33 @@ __global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t
         c.init(odd);
         const uint32_t col = odd ? SPLIT2_MSGS : j;
         __syncthreads();
+        uint64_t tc0 = 0, tr0 = 0;
+        if (PROBE == 3) {
+            tc0 = __builtin_amdgcn_s_memtime();
+            tr0 = __builtin_amdgcn_s_memrealtime();
+        }
+        uint64_t twait = 0;
         for (uint32_t b = 0; b < nbmax; ++b) {
             if (b < nb && PROBE != 2) {
                 const uint64_t (*kb)[SPLIT2_COLS] = kw[b % 3];
                 c.block(h, [&](int t) { return kb[t][col]; });
             }
-            __syncthreads();
+            if (PROBE == 3) {
+                const uint64_t tb = __builtin_amdgcn_s_memtime();
+                __syncthreads();
+                twait += __builtin_amdgcn_s_memtime() - tb;
+            } else {
+                __syncthreads();
+            }
+        }
+        if (PROBE == 3) {   // shader cycles and 100 MHz ticks of the round wave (digest slot of message 0)
+            if (lane == 0) {
+                reinterpret_cast<uint64_t*>(out)[0] = __builtin_amdgcn_s_memtime() - tc0;
+                reinterpret_cast<uint64_t*>(out)[1] = __builtin_amdgcn_s_memrealtime() - tr0;
+                reinterpret_cast<uint32_t*>(out)[4] = __builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+                reinterpret_cast<uint64_t*>(out)[4] = twait;   // cycles waiting at the period barriers
+            }
+            return;
         }
         if (live) {
             // odd lane: a b c d = digest bytes 0..31; even lane: e f g h = bytes 32..63
@@ -311,6 +342,7 @@ __global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t
     }
     // schedule waves: A (wave 1) owns the even blocks, B (wave 2) the odd ones
     const uint32_t par = wave - 1;
+    if (PROBE == 3 && lane == 0) reinterpret_cast<uint32_t*>(out)[4 + wave] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
     RawBlock rb;
     uint64_t w[16];
     const uint32_t k0 = par;                       // first own block

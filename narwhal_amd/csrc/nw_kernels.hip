@@ -18,6 +18,7 @@
 // strict verdict) -> k_slow_prep / k_slow_mul (compacted list of mismatches only) -> k_cert_finalize.
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cstdlib>
 #include "nw_point.h"
 #include "nw_sha512.h"
 #include "nw_kernels.h"
@@ -361,13 +362,18 @@ __global__ void __launch_bounds__(256) k_flags_to_ok(uint32_t n, const uint32_t*
 // direct-sum argument of k_slow_prep cannot decide): one quad per entry, every point operation
 // split over the quad's 4 lanes (nw_quad.h), signed radix-16 digits of the 128-bit z_i with the
 // multiples 1..8 D_i in LDS: 7 table operations + 128 doublings + 32 additions on the quad.
-static constexpr uint32_t SLOW_MUL_QUADS = 16;   // per 64-thread workgroup
-__global__ void __launch_bounds__(64) k_slow_mul(VerifyParams a) {
+// 256-thread workgroups (64 quads) with the entries dealt to the blocks first: an adversarial
+// batch's few hundred entries land on wave 0 of every block, one working wave per CU (one-wave
+// blocks were packed up to three to a SIMD by the dispatcher, stretching the serial chains).
+static constexpr uint32_t SLOW_MUL_QUADS = 64;   // per 256-thread workgroup
+__global__ void __launch_bounds__(256) k_slow_mul(VerifyParams a) {
     __shared__ uint32_t tab[SLOW_MUL_QUADS][8][40];
     const uint32_t cnt = *a.slow_count;
     const uint32_t qd = threadIdx.x >> 2, q = threadIdx.x & 3u;
     uint32_t (*T)[40] = tab[qd];
-    for (uint32_t t = blockIdx.x * SLOW_MUL_QUADS + qd; t < cnt; t += gridDim.x * SLOW_MUL_QUADS) {
+    // entries dealt to the blocks first (one wave each), as in k_slow_prep: a wave's time is one
+    // chain whatever its number of quads, so spreading the entries keeps the waves short and apart
+    for (uint32_t t = qd * gridDim.x + blockIdx.x; t < cnt; t += gridDim.x * SLOW_MUL_QUADS) {
         uint32_t* rec = a.slow_buf + (size_t)t * SLOW_WORDS;
         if (rec[SLOW_KIND] != SK_BIG) continue;                      // uniform over the quad
         const uint32_t i = a.slow_list[t];
@@ -441,7 +447,7 @@ hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint3
     hipError_t e = launch_vs(p, msgmode, key_window, true, n_upper, st);
     if (e != hipSuccess) return e;
     const uint32_t nb = std::min<uint32_t>(blocks_for(n_upper, SLOW_MUL_QUADS), 256u);
-    hipLaunchKernelGGL(k_slow_mul, dim3(nb), dim3(64), 0, st, p);
+    hipLaunchKernelGGL(k_slow_mul, dim3(nb), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 

@@ -129,8 +129,17 @@ hipError_t launch_split_wa(const VerifyParams& p, int msgmode, hipStream_t st);
 // Entries of certificates already rejected (bad S / undecodable A, from k_finish) are skipped.
 template <int MSGMODE, int WA>
 __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
+#ifdef NW_SLOW_TIMING
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+#endif
     const uint32_t cnt = *a.slow_count;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < cnt; t += gridDim.x * blockDim.x) {
+    // Entries are dealt to the blocks first (entry t -> block t mod grid, thread t / grid): the few
+    // thousand entries of an adversarial batch land on wave 0 of every block, one working wave per
+    // CU, instead of filling the first blocks' four waves, which the dispatcher may pack two or three
+    // to a SIMD (each entry is a long serial chain: sharing a SIMD stretched the kernel 3x,
+    // measured at C5 with per-entry timestamps).
+    const uint32_t nthr = gridDim.x * blockDim.x;
+    for (uint32_t t = threadIdx.x * gridDim.x + blockIdx.x; t < cnt; t += nthr) {
         const uint32_t i = a.slow_list[t];
         uint32_t* rec = a.slow_buf + (size_t)t * SLOW_WORDS;
         const uint32_t cert = a.sig_cert[i];
@@ -140,6 +149,9 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
         }
         uint32_t R[8];
         load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
+#ifdef NW_SLOW_TIMING   // variant builds only (tools/build_variants.sh): per-phase shader cycles
+        const uint64_t tm0 = __builtin_amdgcn_s_memtime();
+#endif
         ge_p3 Rp;
         if (!ge_decompress(Rp, R)) {
             a.flags[i] |= NW_F_R_BAD;
@@ -147,6 +159,9 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
             rec[SLOW_KIND] = SK_SKIP;
             continue;
         }
+#ifdef NW_SLOW_TIMING
+        const uint64_t tm1 = __builtin_amdgcn_s_memtime();
+#endif
         ge_p3 P;
         if (a.flags[i] & NW_F_P_SAVED) {
             P = load_p3(a.pslow + (size_t)i * 40);
@@ -155,12 +170,22 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
             lane_inputs<MSGMODE>(a, i, R2, S, slot, kinfo, c2, h);
             P = compute_P<WA>(S, h, true, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
         }
+#ifdef NW_SLOW_TIMING
+        const uint64_t tm2 = __builtin_amdgcn_s_memtime();
+#endif
         const ge_p3 D = ge_add(Rp, ge_cached_neg(ge_to_cached(P)));
         uint32_t z4[4];
         coeff_z(a, i, cert, z4);
         const bool zzero = (z4[0] | z4[1] | z4[2] | z4[3]) == 0;
         const ge_p3 D2 = ge_dbl(D), D4 = ge_dbl(D2);
         const bool small = ge_is_identity(ge_dbl(D4));
+#ifdef NW_SLOW_TIMING
+        const uint64_t tm3 = __builtin_amdgcn_s_memtime();
+        printf("slow_prep t=%u saved=%d dec=%llu P=%llu Dz8=%llu small=%d rt0=%llu rt1=%llu\n", t,
+               (a.flags[i] & NW_F_P_SAVED) ? 1 : 0, (unsigned long long)(tm1 - tm0), (unsigned long long)(tm2 - tm1),
+               (unsigned long long)(tm3 - tm2), small ? 1 : 0, (unsigned long long)rt_start,
+               (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
         const uint32_t kind = (small || zzero) ? SK_SMALL : SK_BIG;
         if (kind == SK_BIG) {
             atomicAdd(&a.cert_state[cert], 1u);

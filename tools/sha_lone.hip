@@ -254,6 +254,22 @@ int main(int argc, char** argv) {
         printf("{\"kernel\": \"%s\", \"blocks\": %u, \"ms\": %.3f, \"ns_per_block\": %.1f, \"worst_ns_per_block\": %.1f}\n",
                names[k], nb, best, best * 1e6 / nb, worst * 1e6 / nb);
     }
+    // split2 launch by launch: wall time, round-wave cycles and the clock they imply
+    for (int rep = 0; rep < 8; ++rep) {
+        CHECK(hipEventRecord(e0, 0));
+        hipLaunchKernelGGL(k_sha512_split2<3>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_dig + 192);
+        CHECK(hipEventRecord(e1, 0));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        uint64_t tt[5];
+        CHECK(hipMemcpy(tt, d_dig + 192, 40, hipMemcpyDeviceToHost));
+        const uint32_t* hw = reinterpret_cast<const uint32_t*>(tt) + 4;   // HW_ID of waves 0, 1, 2
+        printf("{\"split2_rep\": %d, \"ms\": %.3f, \"ns_per_block\": %.1f, \"cycles_per_block\": %.0f, \"clock_ghz\": %.3f, "
+               "\"barrier_wait_per_block\": %.0f, \"simd\": [%u, %u, %u], \"cu\": [%u, %u, %u]}\n",
+               rep, ms, ms * 1e6 / nb, (double)tt[0] / nb, (double)tt[0] / (tt[1] * 10.0), (double)tt[4] / nb, (hw[0] >> 4) & 3,
+               (hw[1] >> 4) & 3, (hw[2] >> 4) & 3, (hw[0] >> 8) & 15, (hw[1] >> 8) & 15, (hw[2] >> 8) & 15);
+    }
     uint8_t dg[192];
     CHECK(hipMemcpy(dg, d_dig, 192, hipMemcpyDeviceToHost));
     printf("{\"split_eq_many\": %s, \"split2_eq_many\": %s}\n", memcmp(dg, dg + 128, 64) ? "false" : "true",
