@@ -417,6 +417,29 @@ class Engine:
                               "nw_verify_batch") == NW_OK
         return call
 
+    def prepare_batches_pk_call(self, counts, msgs, pks, sigs):
+        """Marshal one nw_verify_batches_pk call once (fixed-length numpy messages); returns
+        ``call(zseed, batch_base) -> uint8[nb]`` that only crosses the ABI."""
+        import numpy as np
+        msgs = np.ascontiguousarray(msgs, dtype=np.uint8)
+        pks = np.ascontiguousarray(pks, dtype=np.uint8)
+        sigs = np.ascontiguousarray(sigs, dtype=np.uint8)
+        counts = np.ascontiguousarray(counts, dtype=np.uint32)
+        n, ml = msgs.shape
+        ptrs = (msgs.ctypes.data + np.arange(n, dtype=np.uint64) * ml).astype(np.uint64)
+        lens = np.full(n, ml, dtype=np.uint64)
+        ok = np.zeros(max(len(counts), 1), np.uint8)
+        keep = (msgs, pks, sigs, counts, ptrs, lens)
+        lib, ctx, nb = LIB, self._ctx, len(counts)
+        args = (counts.ctypes.data, ptrs.ctypes.data, lens.ctypes.data, pks.ctypes.data, sigs.ctypes.data)
+
+        def call(zseed: bytes, batch_base: int = 0):
+            _ = keep
+            self.check(lib.nw_verify_batches_pk(ctx, nb, *args, zseed, batch_base, ok.ctypes.data),
+                       "nw_verify_batches_pk")
+            return ok[:nb]
+        return call
+
     def points_sum_is_identity(self, points) -> bool:
         blob = b"".join(bytes(p) for p in points)
         r = ctypes.c_int(0)

@@ -120,6 +120,46 @@ def test_uncached_worker_chunks_vs_oracle(bare):
     assert bare.committee_size() == 0
 
 
+@pytest.mark.parametrize("ragged", [False, True])
+def test_uncached_large_call_vs_small_calls(bare, ragged):
+    """One 20,000-signature nw_verify_batches_pk call (multi-chunk windows in every batch): the
+    verdicts equal those of the same batches verified by 5,000-signature calls with matching batch
+    indices (coefficients are keyed by the global batch index), and the oracle's on a bad and a
+    good chunk.
+    ragged: 8- and 32-byte messages interleaved at random (per-message staging, uneven slices)."""
+    rng = random.Random(77 + ragged)
+    count, nch = 20000, 16
+    seeds = [bytes(rng.randrange(256) for _ in range(32)) for _ in range(count)]
+    msgs = [i.to_bytes(8, "little") * (4 if ragged and rng.random() < 0.5 else 1) for i in range(count)]
+    pks, sigs = [None] * count, [None] * count
+    for ml in (8, 32):   # nw_sign_many signs equal-length messages
+        ix = [i for i in range(count) if len(msgs[i]) == ml]
+        if ix:
+            p_, s_ = bare.sign_many([seeds[i] for i in ix], [msgs[i] for i in ix])
+            for k, i in enumerate(ix):
+                pks[i], sigs[i] = p_[k], s_[k]
+    bad = (5, 4999, 5000, 15001, 19999)
+    for i in bad:
+        s = bytearray(sigs[i])
+        s[40] ^= 4
+        sigs[i] = bytes(s)
+    chunks = [(count * (c + 1)) // nch - (count * c) // nch for c in range(nch)]
+    zseed = bytes(rng.randrange(256) for _ in range(32))
+    got = bare.verify_batches_pk(chunks, msgs, pks, sigs, zseed, 900)
+    firsts = [sum(chunks[:c]) for c in range(nch)]
+    want = [all(not (f <= i < f + n) for i in bad) for f, n in zip(firsts, chunks)]
+    assert got == want
+    small = []
+    for g in range(0, nch, 4):   # 5,000 signatures per call: the unsliced path
+        f0, f1 = firsts[g], firsts[g] + sum(chunks[g:g + 4])
+        small += bare.verify_batches_pk(chunks[g:g + 4], msgs[f0:f1], pks[f0:f1], sigs[f0:f1], zseed, 900 + g)
+    assert small == got
+    for c in (3, 7):
+        f, n = firsts[c], chunks[c]
+        zs = o.batch_coefficients(zseed, 900 + c, n)
+        assert o.verify_batch_z(msgs[f:f + n], sigs[f:f + n], pks[f:f + n], zs) == got[c]
+
+
 @pytest.mark.parametrize("n", [1, 67, 700, 6667])
 def test_uncached_batch_sizes(bare, n):
     """Both MSM window sizes (C = 7 below 512 signatures, 8 above) and multi-chunk windows
