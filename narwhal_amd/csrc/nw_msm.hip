@@ -243,6 +243,11 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
     __shared__ uint32_t s_thru[64];
     const MsmTask task = a.tasks[blockIdx.x];
     const uint32_t L = threadIdx.x;
+#ifdef NW_MSM_TIMING   // variant builds only (tools/build_variants.sh): per-phase shader cycles
+    uint64_t tst[5];
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+    tst[0] = __builtin_amdgcn_s_memtime();
+#endif
     const size_t E = 2 * (size_t)a.nsig;
     const int16_t* dg = a.dig + (size_t)task.win * E + task.e0;
     const uint32_t m = task.e1 - task.e0;   // <= MSM_CH (host-checked)
@@ -254,6 +259,9 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
         if (d) atomicAdd(&cur[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
     }
     __syncthreads();
+#ifdef NW_MSM_TIMING
+    tst[1] = __builtin_amdgcn_s_memtime();
+#endif
     // 2. exclusive scan: lane L owns buckets [L SPL, L SPL + SPL)
     uint32_t loc[SPL];
     uint32_t sum = 0;
@@ -287,6 +295,9 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
         }
     }
     __syncthreads();
+#ifdef NW_MSM_TIMING
+    tst[2] = __builtin_amdgcn_s_memtime();
+#endif
     // 4. balanced accumulation: lane L takes sorted positions [p0, p1)
     const uint32_t q = (total + 63) / 64;
     const uint32_t p0 = min(total, L * q), p1 = min(total, p0 + q);
@@ -322,7 +333,8 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) nx[k] = q2[k];
             }
-            acc = ge_madd(acc, ge_precomp_cneg(ge_precomp_from_words(w), neg));
+            // fused-carry product groups: two waves share each SIMD here (412 vs 424 us per launch)
+            acc = ge_madd<true>(acc, ge_precomp_cneg(ge_precomp_from_words(w), neg));
             const bool last = p + 1 == p1;
             const bool brk = last || (vn >> 16) != cb;   // the run of bucket cb ends here
             if (brk) {
@@ -347,6 +359,9 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
     s_hb[L] = hb;
     s_thru[L] = thru;
     __syncthreads();
+#ifdef NW_MSM_TIMING
+    tst[3] = __builtin_amdgcn_s_memtime();
+#endif
     // 5. merge runs that cross slice boundaries: the lane holding a bucket's first entry adds the
     //    head partials of the following lanes (through-partials continue the chain)
     if (tb >= 0) {
@@ -389,6 +404,14 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
         X = ge_add_p3(X, V);   // lanes >= off add garbage; only lane 0's result is used
     }
     if (L == 0) store_p3(a.wpart + (size_t)task.out * MSM_PT_WORDS, X);
+#ifdef NW_MSM_TIMING
+    tst[4] = __builtin_amdgcn_s_memtime();
+    if (L == 0 && (blockIdx.x % 16) == 0)
+        printf("MSMT %u %u %u %llu %llu %llu %llu %llu %u\n", blockIdx.x, task.win, task.e1 - task.e0,
+               (unsigned long long)rt0, (unsigned long long)(tst[1] - tst[0]), (unsigned long long)(tst[2] - tst[1]),
+               (unsigned long long)(tst[3] - tst[2]), (unsigned long long)(tst[4] - tst[3]),
+               __builtin_amdgcn_s_getreg((31 << 11) | 4));
+#endif
 }
 
 // One wave per (batch, window): sum of the window's chunk partials into slot wfirst[bw].
