@@ -232,17 +232,42 @@ __global__ void __launch_bounds__(256) k_msm_prep(MsmParams a) {
     }
 }
 
+// Tasks per k_msm_bucket workgroup, one per wave.  With one-wave workgroups the dispatcher left
+// some SIMDs with several bucket waves and others with none (per-wave timestamps: the same
+// 1,953-entry accumulation took 146 k to 2.1 M cycles); a 4-wave workgroup spreads over the CU's
+// four SIMDs.
+#ifndef MSM_BUCKET_WAVES
+#define MSM_BUCKET_WAVES 4
+#endif
+
+// Ordering between the lanes of ONE wave at a task's phase boundaries (LDS histogram / cursors /
+// sorted indices, and the global bucket and partial sums that other lanes of the wave wrote):
+// workgroup-scope fences (they wait for the wave's outstanding memory operations) around a
+// wave-level barrier replace __syncthreads, which would couple the block's independent waves.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 template <int C>
-__global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
+__global__ void __launch_bounds__(64 * MSM_BUCKET_WAVES) k_msm_bucket(MsmParams a) {
     constexpr uint32_t B = 1u << (C - 1);   // buckets: digit magnitudes 1..B
     constexpr uint32_t SPL = B / 64;          // buckets per lane in the reduction
     static_assert(SPL >= 1, "at least one bucket per lane");
-    __shared__ uint32_t idx[MSM_CH];
-    __shared__ uint32_t cur[B];
-    __shared__ int32_t s_hb[64];
-    __shared__ uint32_t s_thru[64];
-    const MsmTask task = a.tasks[blockIdx.x];
-    const uint32_t L = threadIdx.x;
+    __shared__ uint32_t idx_w[MSM_BUCKET_WAVES][MSM_CH];
+    __shared__ uint32_t cur_w[MSM_BUCKET_WAVES][B];
+    __shared__ int32_t s_hb_w[MSM_BUCKET_WAVES][64];
+    __shared__ uint32_t s_thru_w[MSM_BUCKET_WAVES][64];
+    // one task per wave; the waves of a block only share the block (no barrier couples them)
+    const uint32_t wv = threadIdx.x >> 6, L = threadIdx.x & 63u;
+    const uint32_t tix = blockIdx.x * MSM_BUCKET_WAVES + wv;
+    if (tix >= a.ntasks) return;
+    uint32_t* idx = idx_w[wv];
+    uint32_t* cur = cur_w[wv];
+    int32_t* s_hb = s_hb_w[wv];
+    uint32_t* s_thru = s_thru_w[wv];
+    const MsmTask task = a.tasks[tix];
 #ifdef NW_MSM_TIMING   // variant builds only (tools/build_variants.sh): per-phase shader cycles
     uint64_t tst[5];
     const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
@@ -252,13 +277,13 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
     const int16_t* dg = a.dig + (size_t)task.win * E + task.e0;
     const uint32_t m = task.e1 - task.e0;   // <= MSM_CH (host-checked)
     for (uint32_t k = L; k < B; k += 64) cur[k] = 0;
-    __syncthreads();
+    wave_lds_sync();
     // 1. histogram of |digit|
     for (uint32_t e = L; e < m; e += 64) {
         const int d = dg[e];
         if (d) atomicAdd(&cur[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
     }
-    __syncthreads();
+    wave_lds_sync();
 #ifdef NW_MSM_TIMING
     tst[1] = __builtin_amdgcn_s_memtime();
 #endif
@@ -278,13 +303,13 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
     }
     const uint32_t total = __shfl(inc, 63, 64);
     uint32_t run = inc - sum;
-    __syncthreads();
+    wave_lds_sync();
 #pragma unroll
     for (uint32_t s = 0; s < SPL; ++s) {
         cur[L * SPL + s] = run;   // cursor; after the scatter it is the bucket's end position
         run += loc[s];
     }
-    __syncthreads();
+    wave_lds_sync();
     // 3. scatter: (bucket << 16) | (negative << 15) | entry offset
     for (uint32_t e = L; e < m; e += 64) {
         const int d = dg[e];
@@ -294,15 +319,15 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
             idx[pos] = (k << 16) | (d < 0 ? 0x8000u : 0u) | e;
         }
     }
-    __syncthreads();
+    wave_lds_sync();
 #ifdef NW_MSM_TIMING
     tst[2] = __builtin_amdgcn_s_memtime();
 #endif
     // 4. balanced accumulation: lane L takes sorted positions [p0, p1)
     const uint32_t q = (total + 63) / 64;
     const uint32_t p0 = min(total, L * q), p1 = min(total, p0 + q);
-    uint32_t* bk = a.bkt + (size_t)blockIdx.x * B * MSM_PT_WORDS;
-    uint32_t* hp = a.part + (size_t)blockIdx.x * 128 * MSM_PT_WORDS;   // head partials [64][40]
+    uint32_t* bk = a.bkt + (size_t)tix * B * MSM_PT_WORDS;
+    uint32_t* hp = a.part + (size_t)tix * 128 * MSM_PT_WORDS;   // head partials [64][40]
     uint32_t* tp = hp + 64 * MSM_PT_WORDS;                               // tail partials [64][40]
     const uint32_t* ent = a.ent + (size_t)task.e0 * MSM_ENT_WORDS;
     int32_t hb = -1, tb = -1;
@@ -358,7 +383,7 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
     }
     s_hb[L] = hb;
     s_thru[L] = thru;
-    __syncthreads();
+    wave_lds_sync();
 #ifdef NW_MSM_TIMING
     tst[3] = __builtin_amdgcn_s_memtime();
 #endif
@@ -374,7 +399,7 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
         }
         store_p3(bk + (uint32_t)tb * MSM_PT_WORDS, acc);
     }
-    __syncthreads();
+    wave_lds_sync();
     // 6. bucket reduction sum_k k S_k (k = magnitude).  Lane L: W_L = sum_s (s+1) S_{L SPL + s},
     //    T_L = sum_s S_{L SPL + s};  total = sum_L W_L + SPL * sum_{L >= 1} U_L with the suffix sums
     //    U_L = sum_{L' >= L} T_L'.
@@ -406,8 +431,8 @@ __global__ void __launch_bounds__(64) k_msm_bucket(MsmParams a) {
     if (L == 0) store_p3(a.wpart + (size_t)task.out * MSM_PT_WORDS, X);
 #ifdef NW_MSM_TIMING
     tst[4] = __builtin_amdgcn_s_memtime();
-    if (L == 0 && (blockIdx.x % 16) == 0)
-        printf("MSMT %u %u %u %llu %llu %llu %llu %llu %u\n", blockIdx.x, task.win, task.e1 - task.e0,
+    if (L == 0 && (tix % 16) == 0)
+        printf("MSMT %u %u %u %llu %llu %llu %llu %llu %u\n", tix, task.win, task.e1 - task.e0,
                (unsigned long long)rt0, (unsigned long long)(tst[1] - tst[0]), (unsigned long long)(tst[2] - tst[1]),
                (unsigned long long)(tst[3] - tst[2]), (unsigned long long)(tst[4] - tst[3]),
                __builtin_amdgcn_s_getreg((31 << 11) | 4));
@@ -493,7 +518,8 @@ static hipError_t launch_msm_c(const MsmParams& p, hipStream_t st) {
         if (e != hipSuccess) return e;
     }
     if (p.ntasks) {
-        hipLaunchKernelGGL(k_msm_bucket<C>, dim3(p.ntasks), dim3(64), 0, st, p);
+        hipLaunchKernelGGL(k_msm_bucket<C>, dim3((p.ntasks + MSM_BUCKET_WAVES - 1) / MSM_BUCKET_WAVES),
+                           dim3(64 * MSM_BUCKET_WAVES), 0, st, p);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
