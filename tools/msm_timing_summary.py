@@ -1,3 +1,4 @@
+"""Per-phase summary of a k_msm_bucket NW_MSM_TIMING run: python tools/msm_timing_summary.py LOG"""
 import sys, collections
 rows=[l.split() for l in open(sys.argv[1]) if l.startswith("MSMT")]
 # keep the last call's launch: rt0 clusters; split by big gaps
