@@ -5,7 +5,7 @@
 // evaluated literally as a segmented Pippenger MSM over the 2n points {R_i, A_i} of every batch:
 //   k_msm_prep     one lane per signature: S parse, R and A decompression, h_i, z_i, a_i = z_i h_i
 //                  mod l, signed radix-2^C digits of z_i and a_i, affine Niels entries;
-//   k_msm_bucket   one wave per (batch, window, chunk of <= MSM_CH entries): LDS counting sort of
+//   k_msm_bucket   one wave per (batch, window, chunk of <= MSM_CH entries), four per workgroup: LDS counting sort of
 //                  the chunk by |digit|, each lane accumulates an equal slice of the sorted list
 //                  (runs that cross slice boundaries are merged afterwards), then the bucket
 //                  reduction sum_k k S_k as per-lane running sums + a cross-lane suffix scan and a
