@@ -169,6 +169,43 @@ def cpu_baseline(cs, com, seconds, probe_seconds=2.5, label="C2"):
                       % (done_certs, int(cs.cert_n[0]), label, done_sigs, dt, threads)}
 
 
+def hashlib_rate(batches, threads, seconds):
+    """Host SHA-512 (hashlib / OpenSSL, releases the GIL) over worker batches on ``threads`` threads:
+    (bytes/s, batches hashed, seconds)."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    n = batches.shape[0]
+    stop = time.perf_counter() + seconds
+
+    def loop(k):
+        nb = 0
+        while time.perf_counter() < stop:
+            hashlib.sha512(batches[(k + nb) % n].data).digest()
+            nb += 1
+        return nb
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        nb = sum(ex.map(loop, range(threads)))
+    dt = time.perf_counter() - t0
+    return nb * batches.shape[1] / dt, nb, dt
+
+
+def cpu_step_with_digests(cb, batches, plan, seconds):
+    """C4 on the host: the rank's signatures at the measured verify rate plus its worker-batch
+    digests at the measured hashlib rate, both on the same threads (one after the other, as one
+    host would have to do both): the CPU counterpart of a C4 step."""
+    bps, nb, dt = hashlib_rate(batches, cb["cores"], seconds)
+    verify_s = plan["sigs"] / cb["value"]
+    digest_s = plan["digest_batches"] * batches.shape[1] / bps
+    return {"hash_GBps": bps / 1e9, "hash_sample": "%d batches of %d B in %.1f s on %d threads (hashlib)"
+                                                    % (nb, batches.shape[1], dt, cb["cores"]),
+            "step_s": verify_s + digest_s, "verify_s": verify_s, "digest_s": digest_s,
+            "sigs_per_s": plan["sigs"] / (verify_s + digest_s),
+            "note": "per-GPU C4 share (%d sigs + %d batches) done by this host: verify at cpu_baseline.value, then "
+                    "the digests at hash_GBps" % (plan["sigs"], plan["digest_batches"])}
+
+
 def host_fed(eng, cs, slots, zseed, chunks=8, threads=4, reps=5):
     """C2 through nw_verify_certs from host buffers: ``chunks`` calls over ``threads`` host threads,
     so one call's host->device copy overlaps another's kernels (each call has its own stream)."""
@@ -206,7 +243,6 @@ def digest_leg(eng, dev, n_node, n_share, reps, cpu_seconds, verify_step):
     sequential SHA-512 compression chain)."""
     import hashlib
     import torch
-    from concurrent.futures import ThreadPoolExecutor
     from narwhal_amd import workload
     out = {}
     host = workload.worker_batches_np(n_node)
@@ -314,21 +350,9 @@ def digest_leg(eng, dev, n_node, n_share, reps, cpu_seconds, verify_step):
     del d_small, q_off, q_len, q_out
     if cpu_seconds > 0:
         threads = max(cpu_thread_candidates())
-        stop = time.perf_counter() + cpu_seconds
-
-        def hash_loop(k):
-            nb = 0
-            while time.perf_counter() < stop:
-                hashlib.sha512(host[(k + nb) % n_node].data).digest()
-                nb += 1
-            return nb
-
-        t0 = time.perf_counter()
-        with ThreadPoolExecutor(threads) as ex:
-            nb = sum(ex.map(hash_loop, range(threads)))
-        dt = time.perf_counter() - t0
-        out["cpu_baseline"] = {"GBps": nb * blen / dt / 1e9, "cores": threads, "kind": "hashlib (OpenSSL) SHA-512",
-                               "per_gpu_share_GBps": nb * blen / dt / 1e9 / GPUS_PER_NODE,
+        bps, nb, dt = hashlib_rate(host, threads, cpu_seconds)
+        out["cpu_baseline"] = {"GBps": bps / 1e9, "cores": threads, "kind": "hashlib (OpenSSL) SHA-512",
+                               "per_gpu_share_GBps": bps / 1e9 / GPUS_PER_NODE,
                                "sample": "%d batches in %.1f s on %d threads" % (nb, dt, threads)}
     return out
 
@@ -569,8 +593,10 @@ def main(argv=None):
     if world != args.gpus and rank == 0:
         print("note: --gpus %d but WORLD_SIZE %d; using WORLD_SIZE" % (args.gpus, world), file=sys.stderr)
     torch.cuda.set_device(local)
+    gloo_group = None
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        gloo_group = dist.new_group(backend="gloo")   # host-side barrier for the CPU-baseline leg
 
     from narwhal_amd import _lib, workload
     plan = config_plan(args, world, rank)
@@ -731,12 +757,22 @@ def main(argv=None):
         if world == 1 and c2 and args.digest_batches > 0:
             out["digest"] = digest_leg(eng, dev, args.digest_batches, args.digest_share, 3,
                                        0.0 if args.no_cpu_baseline else 3.0, verify_step)
-        if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(cs, com, args.cpu_seconds, label=args.config)
+        if not args.no_cpu_baseline:
+            # every line carries the host baseline, N > 1 included: rank 0 times it after the timed
+            # region while the other ranks block in a gloo barrier (a socket wait, no spinning host
+            # thread to steal the cores being measured)
+            cb = cpu_baseline(cs, com, args.cpu_seconds, label=args.config)
+            if ndig:
+                cb["with_digests"] = cpu_step_with_digests(cb, host_b, plan, args.cpu_seconds / 3)
+            cb["gpu_over_cpu"] = value / cb["value"]
+            if ndig:
+                cb["with_digests"]["gpu_over_cpu"] = value / cb["with_digests"]["sigs_per_s"]
+            out["cpu_baseline"] = cb
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     if world > 1:
+        dist.barrier(group=gloo_group)    # ranks > 0 wait here while rank 0 times the host baseline
         dist.barrier()
         dist.destroy_process_group()
     return 0

@@ -15,6 +15,7 @@
 //     kernel may still read it.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -160,7 +161,6 @@ struct nw_ctx {
     int device = 0;
     hipStream_t stream = nullptr;   // administrative stream: basepoint table, committee loads
     uint32_t finish_k = 0;          // k_finish signatures per lane (0: adaptive, finish_k_for)
-    bool group_off = false;         // NW_GROUP=0: never sort signatures by signer (A/B knob)
     // key cache (shared by all calls; guarded by keys_mu)
     std::shared_mutex keys_mu;
     uint32_t* d_btab = nullptr;
@@ -294,16 +294,19 @@ const uint8_t kBaseEnc[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x
                               0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                               0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
 
-// k_finish signatures per lane (NW_FK overrides it for tuning; 1..FINISH_K).  Measured on MI355X:
-// splitting a batch into chunks so k_finish of one chunk overlaps k_verify of the next on a second
-// stream was slower (623 vs 712 M sigs/s at C2: the co-running k_finish waves take VGPR slots from
-// the VALU-bound k_verify and every chunk pays a tail), so a batch is one k_verify + one k_finish.
-// NW_FK = 0 (default): adaptive, see finish_k_for.
-uint32_t finish_k() {
-    const char* e = std::getenv("NW_FK");
-    const long k = e ? std::strtol(e, nullptr, 10) : 0;
-    return k >= 1 && k <= FINISH_K ? (uint32_t)k : 0u;
-}
+// k_finish signatures per lane: adaptive (finish_k_for); variant builds for A/B runs may pin it with
+// -DNW_FK_FIXED=k (tools/build_variants.sh).  Measured on MI355X: splitting a batch into chunks so
+// k_finish of one chunk overlaps k_verify of the next on a second stream was slower (623 vs 712 M
+// sigs/s at C2: the co-running k_finish waves take VGPR slots from the VALU-bound k_verify and every
+// chunk pays a tail), so a batch is one k_verify + one k_finish.
+#ifndef NW_FK_FIXED
+#define NW_FK_FIXED 0
+#endif
+static_assert(NW_FK_FIXED >= 0 && NW_FK_FIXED <= FINISH_K, "NW_FK_FIXED: 0 (adaptive) or 1..FINISH_K");
+// Signer grouping on (1, release) or off (0: variant builds for the A/B of the grouping itself).
+#ifndef NW_GROUP_SIGNERS
+#define NW_GROUP_SIGNERS 1
+#endif
 
 // Signatures per k_finish lane for a launch of n: just enough that the lanes fit one wave per SIMD
 // (256 CUs x 4 SIMDs x 64 lanes), because below that the kernel is bound by the serial
@@ -480,6 +483,20 @@ struct PreStaged {
 constexpr size_t kStagedMaxSigs = 16384;
 static_assert(kStagedMaxSigs <= kGroupMinSigs, "staged calls never group");
 
+// Certificate / batch vote ranges must be pairwise disjoint: a vote belongs to at most one
+// certificate (its coefficient z and its exact-path term are keyed by that certificate).  Empty
+// ranges never overlap anything.
+bool ranges_disjoint(const uint32_t* first, const uint32_t* nv, size_t n) {
+    std::vector<std::pair<uint64_t, uint64_t>> r;
+    r.reserve(n);
+    for (size_t c = 0; c < n; ++c)
+        if (nv[c]) r.emplace_back(first[c], (uint64_t)first[c] + nv[c]);
+    std::sort(r.begin(), r.end());
+    for (size_t k = 1; k < r.size(); ++k)
+        if (r[k].first < r[k - 1].second) return false;
+    return true;
+}
+
 // Bytes of the PreStaged block for a call (256-B aligned segments).
 size_t prestaged_bytes(size_t nsigs, size_t ncerts) {
     return align256((nsigs + 1) * 4) + 256 + align256(ncerts * 4 + 4);
@@ -491,7 +508,8 @@ void prestage(uint8_t* h, uint8_t* d, const uint32_t* first, const uint32_t* nv,
     const size_t o_sc = 0, o_z = align256((nsigs + 1) * 4), o_cs = o_z + 256;
     uint32_t* sc = reinterpret_cast<uint32_t*>(h + o_sc);
     std::memset(h, 0, prestaged_bytes(nsigs, ncerts));
-    for (size_t c = 0; c < ncerts; ++c) {   // host-validated ranges: inside [0, nsigs)
+    std::memset(h + o_sc, 0xFF, (nsigs + 1) * 4);   // NO_CERT: votes outside every range
+    for (size_t c = 0; c < ncerts; ++c) {   // host-validated ranges: inside [0, nsigs), disjoint
         const size_t f = first[c], e = f + nv[c];
         for (size_t v = f; v < e; ++v) sc[v] = (uint32_t)c;
     }
@@ -508,7 +526,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
                   const uint8_t* d_msg_base, const uint64_t* d_msg_off, const uint64_t* d_msg_len,
                   const uint8_t* zseed, uint64_t cert_base, uint32_t batch_mode, uint8_t* d_cert_ok,
                   uint32_t* d_flags_user, uint64_t* d_stake_out, hipStream_t st, uint8_t* d_sig_ok = nullptr,
-                  uint32_t* d_status = nullptr, const PreStaged* pre = nullptr) {
+                  uint32_t* d_status = nullptr, const PreStaged* pre = nullptr, bool sync_check = false) {
     uint32_t* d_flags = d_flags_user;
     if (!d_flags) {
         NW_TRY(ws->ensure(ws->w_flags, nsigs * 4 + 4), "ws flags");
@@ -527,7 +545,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     NW_TRY(ws->ensure(ws->w_pbuf, nsigs * (size_t)PBUF_WORDS * 4 + 16), "ws pbuf");
     NW_TRY(ws->ensure(ws->w_pre, nsigs * 40 + 16), "ws pre");
     // signer grouping (device counting sort) when keys repeat
-    const bool group = !pre && !ctx->group_off && nsigs >= kGroupMinSigs && ctx->nkeys > 1 &&
+    const bool group = NW_GROUP_SIGNERS && !pre && nsigs >= kGroupMinSigs && ctx->nkeys > 1 &&
                        nsigs >= kGroupMinSigsPerKey * ctx->nkeys;
     if (group) {
         NW_TRY(ws->ensure(ws->w_counts, ctx->nkeys * 4 + 16), "ws counts");
@@ -538,13 +556,30 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     uint32_t* slow_count = pre ? pre->zero4 : ws->w_slow_count.as<uint32_t>();
     uint32_t* cert_state = !batch_mode ? nullptr : (pre ? pre->cert_state : ws->w_cert_state.as<uint32_t>());
     if (!pre) {
-        // Preamble in two launches: zero sig_cert (votes outside every certificate map to certificate
-        // 0), the slot counts, the slow-path counter, the certificate states and d_status; expand
-        // certificates; histogram signer slots; check the device inputs into d_status (when given).
+        // Preamble in two launches: sig_cert = NO_CERT, zero the slot counts, the slow-path counter,
+        // the certificate states and the status word; expand certificates; histogram signer slots;
+        // check the device inputs into the status word.  sync_check: the call waits for that check
+        // and returns NW_ERR_ARG before anything else is enqueued.
+        if (sync_check) {
+            NW_TRY(ws->ensure(ws->w_status, 16), "ws status");
+            d_status = ws->w_status.as<uint32_t>();
+        }
         NW_TRY(launch_prep_expand((uint32_t)ncerts, (uint32_t)nsigs, (uint32_t)ctx->nkeys, d_first, d_nv, d_signer,
                                   sig_cert, slow_count, group ? ws->w_counts.as<uint32_t>() : nullptr, d_status,
                                   cert_state, st),
                "k_prep_certs / k_expand_count");
+        if (sync_check) {
+            NW_TRY(ws->h_io.ensure(16), "pinned status");
+            NW_TRY(hipMemcpyAsync(ws->h_io.p, d_status, 4, hipMemcpyDeviceToHost, st), "D2H status");
+            NW_TRY(hipStreamSynchronize(st), "sync(status)");
+            uint32_t sv = 0;
+            std::memcpy(&sv, ws->h_io.p, 4);
+            if (sv != 0) {
+                set_error(ctx, "nw_verify_certs_dev: vote range past nsigs, overlapping vote ranges, or signer slot "
+                               "outside the key cache");
+                return NW_ERR_ARG;
+            }
+        }
     }
 
     VerifyParams vp{};
@@ -616,6 +651,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     fp.cert_n = d_nv;
     fp.flags = d_flags;
     fp.signer = d_signer;
+    fp.sig_cert = sig_cert;
     fp.stake = ctx->d_stake;
     fp.slow_slot = vp.slow_slot;
     fp.slow_buf = vp.slow_buf;
@@ -983,11 +1019,7 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
         return NW_ERR_ARG;
     nw_ctx* ctx = new nw_ctx();
     ctx->device = dev;
-    ctx->finish_k = finish_k();
-    {
-        const char* g = std::getenv("NW_GROUP");
-        ctx->group_off = g && g[0] == '0';
-    }
+    ctx->finish_k = NW_FK_FIXED;
     if (opts && opts->max_keys) {
         ctx->max_keys = opts->max_keys;
         ctx->max_keys_user = true;
@@ -1232,6 +1264,10 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
     }
     if (nsigs > 0xFFFFFFF0u) return NW_ERR_ARG;
     if (nsigs && (!sig || !signer_slot)) return NW_ERR_ARG;
+    if (!ranges_disjoint(first.data(), nv.data(), ncerts)) {
+        set_error(ctx, "overlapping certificate vote ranges");
+        return NW_ERR_ARG;
+    }
     std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);
     for (size_t v = 0; v < nsigs; ++v)
         if (signer_slot[v] >= ctx->nkeys) {
@@ -1308,6 +1344,10 @@ int nw_verify_batches(nw_ctx* ctx, size_t nb, const uint32_t* first, const uint3
     }
     if (nsigs > 0xFFFFFFF0u) return NW_ERR_ARG;
     if (nsigs && (!sig || !signer_slot || !msg || !len)) return NW_ERR_ARG;
+    if (!ranges_disjoint(first, nvotes, nb)) {
+        set_error(ctx, "overlapping batch ranges");
+        return NW_ERR_ARG;
+    }
     std::shared_lock<std::shared_mutex> keys(ctx->keys_mu);
     for (size_t v = 0; v < nsigs; ++v)
         if (signer_slot[v] >= ctx->nkeys) {
@@ -1369,31 +1409,17 @@ int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first
     Workspace* ws = lease.ws();
     if (!ws) return NW_ERR_DEVICE;
     NW_TRY(lease.bind(st, false), "hipStreamWaitEvent");
-    // input validation on the device (the inputs are device-resident); every kernel below also
-    // clamps them, so invalid inputs never fault
-    // With d_status the check runs inside the batch preamble (k_expand_count) in stream order;
-    // without it the call validates first and waits for the verdict.
-    if (!d_status) {   // synchronous validation: NW_ERR_ARG before any verification is enqueued
-        NW_TRY(ws->ensure(ws->w_status, 16), "ws status");
-        uint32_t* status = ws->w_status.as<uint32_t>();
-        NW_TRY(hipMemsetAsync(status, 0, 4, st), "memset status");
-        NW_TRY(launch_validate_certs((uint32_t)ncerts, (uint32_t)nsigs, (uint32_t)ctx->nkeys, d_cert_first,
-                                     d_cert_nvotes, d_signer_slot, status, st),
-               "k_validate_certs");
-        NW_TRY(ws->h_io.ensure(16), "pinned status");
-        NW_TRY(hipMemcpyAsync(ws->h_io.p, status, 4, hipMemcpyDeviceToHost, st), "D2H status");
-        NW_TRY(hipStreamSynchronize(st), "sync(status)");
-        uint32_t sv = 0;
-        std::memcpy(&sv, ws->h_io.p, 4);
-        if (sv != 0) {
-            set_error(ctx, "nw_verify_certs_dev: vote range past nsigs or signer slot outside the key cache");
-            lease.synced();
-            return NW_ERR_ARG;
-        }
-    }
+    // Input validation on the device (the inputs are device-resident) inside the batch preamble
+    // (k_expand_count): with d_status it is written there in stream order; without it the call waits
+    // for the check and returns NW_ERR_ARG before any verification is enqueued.  Every kernel also
+    // clamps the inputs, so invalid inputs never fault.
     int rc = enqueue_certs(ctx, ws, ncerts, d_cert_first, d_cert_nvotes, nsigs, d_sig64, d_signer_slot, 0, d_msg32,
                            nullptr, nullptr, nullptr, zseed, cert_base, 1, d_cert_ok, d_sig_flags, d_accepted_stake,
-                           st, nullptr, d_status);
+                           st, nullptr, d_status, nullptr, d_status == nullptr);
+    if (rc == NW_ERR_ARG) {
+        lease.synced();
+        return rc;
+    }
     NW_TRY(lease.finish(), "hipEventRecord");
     return rc;
 }

@@ -8,15 +8,13 @@
 //
 //  * k_sha512_many  - one lane per message, everything in one wave: the throughput form (enough
 //                     messages to give every SIMD several waves).
-//  * k_sha512_split - few messages (worker batches: 1,250 per GPU at C4, a 6,667-parent header):
-//                     the message schedule does not depend on the chaining state, so a second wave
-//                     of the same workgroup computes K_t + W_t of block b+1 into LDS while the first
-//                     runs the 80 rounds of block b from LDS.  The round wave issues 27 VALU
-//                     instructions per round (Sigma1 8, Ch 2, Sigma0 8, Maj 2, 7 adds) + one LDS read,
-//                     instead of ~43 with the schedule inline; the two waves meet at one barrier per
-//                     block.
+//  * k_sha512_split2 - few messages (worker batches: 1,250 per GPU at C4, a 6,667-parent header):
+//                     the message schedule does not depend on the chaining state, so two schedule
+//                     waves of the same workgroup compute K_t + W_t of the next blocks into LDS while
+//                     the round wave runs the 80 rounds of block b from LDS, each message on a lane
+//                     pair (nw_sha512_2l.h: 20 VALU instructions per round for both halves of the
+//                     chain); the waves meet at one barrier per block.
 #include <hip/hip_runtime.h>
-#include <cstdlib>
 #include "nw_sha512.h"
 #include "nw_sha512_2l.h"
 #include "nw_kernels.h"
@@ -45,7 +43,7 @@ __device__ __forceinline__ void sha512_load_block(const uint8_t* m, uint64_t L, 
     const int32_t v = vrem <= 0 ? 0 : (vrem >= 128 ? 128 : (int32_t)vrem);
     const bool marker = vrem >= 0 && vrem < 128;                // the 0x80 byte lands in this block
     uint32_t u[33];
-    if (v + (int32_t)sh > 0) {
+    if (v > 0) {   // a padding-only block (v == 0) reads nothing: its q[0] may lie past the message
         const int32_t kmax = (v + (int32_t)sh - 1) >> 2;          // last dword with a valid byte
 #pragma unroll
         for (int k = 0; k < 33; ++k) u[k] = q[k < kmax ? k : kmax];
@@ -99,111 +97,11 @@ __global__ void __launch_bounds__(256, 4) k_sha512_many(uint32_t n, const uint8_
 }
 
 // ------------------------------------------------------------------------------------ schedule / round split
-static constexpr uint32_t SPLIT_MSGS = 64;        // messages per workgroup: lane L of both waves
 static constexpr uint32_t SPLIT_MAX_N = 32768;    // above: k_sha512_many (every SIMD has work anyway)
 
-// t1 = h + (K_t + W_t) + Sigma1(e) + Ch(e, f, g); t2 = Sigma0(a) + Maj(a, b, c)
-#define NW_SHA_ROUND_KW(a, b, c, d, e, f, g, h, kw)                                                     \
-    do {                                                                                                \
-        const uint64_t t1 = (h) + (kw) + xor3_64(rotr64((e), 14), rotr64((e), 18), rotr64((e), 41)) +     \
-                            ch64((e), (f), (g));                                                        \
-        const uint64_t t2 = xor3_64(rotr64((a), 28), rotr64((a), 34), rotr64((a), 39)) + maj64((a), (b), (c)); \
-        (d) += t1;                                                                                      \
-        (h) = t1 + t2;                                                                                  \
-    } while (0)
-
-// Schedule wave: K_t + W_t for t = 0..79 of block b into kwb[t][lane].
-__device__ __forceinline__ void split_schedule(const uint8_t* m, uint64_t L, uint64_t b, uint64_t (*kwb)[SPLIT_MSGS],
-                                               uint32_t lane) {
-    uint64_t w[16];
-    sha512_load_block(m, L, b, w);
-#pragma unroll
-    for (int t = 0; t < 16; ++t) kwb[t][lane] = w[t] + SHA512_K[t];
-#pragma unroll
-    for (int r = 16; r < 80; r += 16) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
-            const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
-            const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
-            w[i] += s0 + w[(i + 9) & 15] + s1;
-            kwb[r + i][lane] = w[i] + SHA512_K[r + i];
-        }
-    }
-}
-
-// Round wave: the 80 rounds of one block with K_t + W_t from LDS (16 words loaded one group ahead).
-__device__ __forceinline__ void split_rounds(uint64_t st[8], const uint64_t (*kwb)[SPLIT_MSGS], uint32_t lane) {
-    uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
-    uint64_t k0[16], k1[16];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) k0[q] = kwb[q][lane];
-#pragma unroll
-    for (int grp = 0; grp < 5; ++grp) {
-        if (grp < 4) {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) k1[q] = kwb[(grp + 1) * 16 + q][lane];
-        }
-        NW_SHA_ROUND_KW(a, b, c, d, e, f, g, h, k0[0]);
-        NW_SHA_ROUND_KW(h, a, b, c, d, e, f, g, k0[1]);
-        NW_SHA_ROUND_KW(g, h, a, b, c, d, e, f, k0[2]);
-        NW_SHA_ROUND_KW(f, g, h, a, b, c, d, e, k0[3]);
-        NW_SHA_ROUND_KW(e, f, g, h, a, b, c, d, k0[4]);
-        NW_SHA_ROUND_KW(d, e, f, g, h, a, b, c, k0[5]);
-        NW_SHA_ROUND_KW(c, d, e, f, g, h, a, b, k0[6]);
-        NW_SHA_ROUND_KW(b, c, d, e, f, g, h, a, k0[7]);
-        NW_SHA_ROUND_KW(a, b, c, d, e, f, g, h, k0[8]);
-        NW_SHA_ROUND_KW(h, a, b, c, d, e, f, g, k0[9]);
-        NW_SHA_ROUND_KW(g, h, a, b, c, d, e, f, k0[10]);
-        NW_SHA_ROUND_KW(f, g, h, a, b, c, d, e, k0[11]);
-        NW_SHA_ROUND_KW(e, f, g, h, a, b, c, d, k0[12]);
-        NW_SHA_ROUND_KW(d, e, f, g, h, a, b, c, k0[13]);
-        NW_SHA_ROUND_KW(c, d, e, f, g, h, a, b, k0[14]);
-        NW_SHA_ROUND_KW(b, c, d, e, f, g, h, a, k0[15]);
-        if (grp < 4) {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) k0[q] = k1[q];
-        }
-    }
-    st[0] += a; st[1] += b; st[2] += c; st[3] += d;
-    st[4] += e; st[5] += f; st[6] += g; st[7] += h;
-}
-
-// 128 threads: wave 0 = rounds, wave 1 = schedule; lane L of both waves serves message
-// 64 * blockIdx.x + L.  kw is double-buffered: while wave 0 compresses block b from kw[b & 1],
-// wave 1 fills kw[(b + 1) & 1]; one barrier per block.  Both waves derive the same trip count (the
-// largest block count of the workgroup's messages), so every barrier is reached by both.
-__global__ void __launch_bounds__(128) k_sha512_split(uint32_t n, const uint8_t* base, const uint64_t* off,
-                                                      const uint64_t* len, uint8_t* out) {
-    __shared__ uint64_t kw[2][80][SPLIT_MSGS];    // 81,920 B: two workgroups per CU
-    const uint32_t lane = threadIdx.x & 63u;
-    const bool sched = threadIdx.x >= 64;         // wave-uniform
-    const uint32_t i = blockIdx.x * SPLIT_MSGS + lane;
-    const bool live = i < n;
-    const uint64_t L = live ? len[i] : 0;
-    const uint8_t* m = base + (live ? off[i] : 0);
-    const uint32_t nb = live ? sha512_nblocks(L) : 0u;
-    uint32_t nbmax = nb;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, o, 64));
-    if (sched && nb > 0) split_schedule(m, L, 0, kw[0], lane);
-    __syncthreads();
-    uint64_t st[8];
-    sha512_init(st);
-    for (uint32_t b = 0; b < nbmax; ++b) {
-        if (sched) {
-            if (b + 1 < nb) split_schedule(m, L, b + 1, kw[(b + 1) & 1], lane);
-        } else if (b < nb) {
-            split_rounds(st, kw[b & 1], lane);
-        }
-        __syncthreads();
-    }
-    if (!sched && live) sha512_digest_store(out + (size_t)i * 64, st);
-}
-
 // ------------------------------------------------------------------------------------ two-lane split
-// k_sha512_split with the rounds on lane pairs (nw_sha512_2l.h: 20 instructions per round for one
-// message instead of 27): 32 messages per workgroup; lane pair (2j, 2j+1) of the round wave serves
+// The rounds on lane pairs (nw_sha512_2l.h: 20 instructions per round for one message instead of
+// the one-lane form's 27): 32 messages per workgroup; lane pair (2j, 2j+1) of the round wave serves
 // message j.
 //
 // At ~3.1 us per block for the rounds, one schedule wave (~3 us of arithmetic per block plus its
@@ -374,14 +272,9 @@ __global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t
 hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                               uint8_t* out, hipStream_t st) {
     if (n == 0) return hipSuccess;
-    static const bool nosplit = std::getenv("NW_SHA_NOSPLIT") != nullptr;   // A/B knobs (tools/)
-    static const bool split1 = std::getenv("NW_SHA_SPLIT1") != nullptr;
-    if (n <= SPLIT_MAX_N && !nosplit) {
-        if (split1)
-            hipLaunchKernelGGL(k_sha512_split, dim3(blocks_for(n, SPLIT_MSGS)), dim3(128), 0, st, n, base, off, len, out);
-        else
-            hipLaunchKernelGGL(k_sha512_split2<0>, dim3(blocks_for(n, SPLIT2_MSGS)), dim3(192), 0, st, n, base, off, len,
-                               out);
+    if (n <= SPLIT_MAX_N) {
+        hipLaunchKernelGGL(k_sha512_split2<0>, dim3(blocks_for(n, SPLIT2_MSGS)), dim3(192), 0, st, n, base, off, len,
+                           out);
     } else {
         hipLaunchKernelGGL(k_sha512_many, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, base, off, len, out);
     }

@@ -24,8 +24,12 @@ static constexpr uint32_t SK_MUL = 3;             // SK_BIG whose z_i D_i was co
 // the certificate is known to be rejected (a vote with bad S / undecodable A / undecodable R).
 static constexpr uint32_t CS_DOOM = 0x80000000u;
 static constexpr uint32_t CS_BIG_MASK = 0x7FFFFFFFu;
-// internal flag bit: k_verify parked P_i (extended) in pslow[i] (its y did not match R's)
+// internal flag bit: k_verify parked P_i (extended) in pslow[i] (its y did not match R's); cleared
+// by k_slow_prep before the flags reach the caller (every such signature is on the slow list)
 static constexpr uint32_t NW_F_P_SAVED = 0x4000u;
+// sig_cert value of a signature inside no certificate's vote range: it gets no verdict (flags 0)
+// and never touches any certificate's exact-path state
+static constexpr uint32_t NO_CERT = 0xFFFFFFFFu;
 static constexpr int PBUF_WORDS = 21;             // per-signature k_verify -> k_finish record (X, Z, flags)
 #ifndef NW_FINISH_K
 #define NW_FINISH_K 16
@@ -41,7 +45,7 @@ struct VerifyParams {
     uint32_t batch_mode;           // 0: strict flags only; 1: batch bookkeeping (z, slow list)
     const uint8_t* sig;            // [n][64]  R || S
     const uint32_t* signer;        // [n] key-cache slot
-    const uint32_t* sig_cert;      // [n] certificate / batch index (local)
+    const uint32_t* sig_cert;      // [n] certificate / batch index (local), NO_CERT outside every range
     const uint32_t* cert_first;    // [ncerts] first signature of each certificate
     const uint8_t* cert_msg;       // MSGMODE 0: [ncerts][32]
     const uint8_t* msg_base;       // MSGMODE 1: packed messages
@@ -76,6 +80,7 @@ struct FinalizeParams {
     const uint32_t* flags;
     const uint32_t* signer;
     const uint32_t* stake;         // [K]
+    const uint32_t* sig_cert;      // [nsigs] owner certificate of each vote (NO_CERT: none)
     const uint32_t* slow_slot;
     const uint32_t* slow_buf;
     const uint32_t* cert_state;    // [ncerts] CS_*
@@ -93,16 +98,15 @@ hipError_t launch_finish(const VerifyParams& p, hipStream_t st);
 // entries); both read the device slow counter, so honest batches find no work.
 hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st);
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st);
-// Batch preamble: zero sig_cert / counts (may be null: no histogram) / the slow counter / status (may
-// be null: no input check), expand certificates, histogram + check signer slots (k_prep_certs,
-// k_expand_count); then launch_group_scatter (scan + scatter) when counts were built.
+// Batch preamble: reset sig_cert to NO_CERT, zero counts (may be null: no histogram) / the slow
+// counter / status (may be null: no input check), expand certificates (a vote claimed by two
+// certificates is NW_ERR_ARG), histogram + check signer slots (k_prep_certs, k_expand_count); then
+// launch_group_scatter (scan + scatter) when counts were built.
 hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
                               const uint32_t* nv, const uint32_t* signer, uint32_t* sig_cert, uint32_t* zero4,
                               uint32_t* counts, uint32_t* status, uint32_t* cert_state, hipStream_t st);
 hipError_t launch_group_scatter(uint32_t n, uint32_t nkeys, const uint32_t* signer, const uint32_t* counts,
                                 uint32_t* cursor, uint32_t* perm, hipStream_t st);
-hipError_t launch_validate_certs(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
-                                 const uint32_t* nv, const uint32_t* signer, uint32_t* status, hipStream_t st);
 hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hipStream_t st);
 hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
                            uint32_t* tab, int window, hipStream_t st);

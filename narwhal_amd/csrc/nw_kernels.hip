@@ -152,10 +152,13 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
             const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
             uint32_t f = finish_x_flags(load_fe_soa(a.pbuf, n, g), zi, a.pbuf[PREC_FLAGS_ROW * n + g]);
             if (a.batch_mode) {
-                if ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) {
+                const uint32_t cert = a.sig_cert[i];
+                if (cert == NO_CERT) {
+                    f = 0u;   // inside no certificate's range: no message, no verdict, no exact-path entry
+                } else if ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) {
                     // the certificate is rejected (dalek: parse / decode error before the MSM): no
                     // exact-path work for any of its votes
-                    atomicOr(&a.cert_state[a.sig_cert[i]], CS_DOOM);
+                    atomicOr(&a.cert_state[cert], CS_DOOM);
                 } else if (!(f & NW_F_MATCH)) {
                     f |= NW_F_SLOW;
                     const uint32_t t = atomicAdd(a.slow_count, 1u);
@@ -239,17 +242,26 @@ __global__ void __launch_bounds__(64) k_cert_exact(FinalizeParams a) {
         const uint32_t c = a.exact_list[e];
         const uint32_t first = a.cert_first[c], nv = a.cert_n[c];   // in range: bad ranges never get listed
         ge_p3 acc = ge_to_vgpr(ge_identity());
-        bool has = false;
+        bool has = false, bad = false;
         uint32_t tsum = 0;
         for (uint32_t v = lane; v < nv; v += 64) {
             const uint32_t f = a.flags[first + v];
             tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
             if (f & NW_F_SLOW) {
-                const ge_p3 q = load_p3(a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS);
+                const uint32_t* rec = a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS;
+                // a term must be final and this certificate's own (valid calls always satisfy both;
+                // a vote claimed by two certificates is NW_ERR_ARG and must not be accepted here)
+                const uint32_t kind = rec[SLOW_KIND];
+                if (a.sig_cert[first + v] != c || (kind != SK_SMALL && kind != SK_MUL)) {
+                    bad = true;
+                    continue;
+                }
+                const ge_p3 q = load_p3(rec);
                 acc = has ? ge_add(acc, ge_to_cached(q)) : q;
                 has = true;
             }
         }
+        bad = __any(bad);
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) tsum += __shfl_xor(tsum, off, 64);
         const uint32_t tk = tsum & 7u;
@@ -271,38 +283,28 @@ __global__ void __launch_bounds__(64) k_cert_exact(FinalizeParams a) {
             const ge_p3 o = ge_shfl_down(acc, off);
             acc = ge_select(acc, ge_add(acc, ge_to_cached(o)), lane + off < k);
         }
-        if (lane == 0 && a.cert_ok) a.cert_ok[c] = ge_is_identity(acc) ? 1 : 0;
+        if (lane == 0 && a.cert_ok) a.cert_ok[c] = (!bad && ge_is_identity(acc)) ? 1 : 0;
     }
-}
-
-// Device-side input check of nw_verify_certs_dev: every vote range inside [0, nsigs) and every
-// signer slot inside the key cache; *status |= NW_ERR_ARG otherwise (the verify kernels clamp the
-// same inputs, so a bad call never reads outside its arrays).
-__global__ void __launch_bounds__(256) k_validate_certs(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys,
-                                                        const uint32_t* cert_first, const uint32_t* cert_n,
-                                                        const uint32_t* signer, uint32_t* status) {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    bool bad = false;
-    if (t < ncerts) bad = (uint64_t)cert_first[t] + cert_n[t] > nsigs;
-    if (t < nsigs) bad = bad || signer[t] >= nkeys;
-    if (bad) atomicOr(status, (uint32_t)NW_ERR_ARG);
 }
 
 // ------------------------------------------------------------------------------------ batch preamble
 // Two launches replace the five small ones a certificate batch used to start with (status /
 // sig_cert / slot-count fills, input check, certificate expansion, slot histogram): ~5 us each on
 // MI355X, dominated by dispatch, not work.
-//   k_prep_certs:   sig_cert = 0 (votes outside every certificate map to certificate 0), the slot
-//                   counts, the slow-path counter and the status word = 0.
-//   k_expand_count: block b expands certificates [4 b, 4 b + 4) into sig_cert and, for
+//   k_prep_certs:   sig_cert = NO_CERT (a vote outside every certificate gets no verdict and no
+//                   exact-path entry), the slot counts, the slow-path counter and the status word = 0.
+//   k_expand_count: block b expands certificates [4 b, 4 b + 4) into sig_cert (a vote already
+//                   claimed by another certificate is NW_ERR_ARG: ranges must be disjoint) and, for
 //                   signature tile b (GROUP_TILE signatures), histograms the signer slots (LDS, one
 //                   global add per slot) and/or checks them; every check ORs NW_ERR_ARG into status.
+//   Device inputs are checked here and nowhere else: vote ranges inside [0, nsigs), pairwise
+//   disjoint, signer slots inside the key cache.
 __global__ void __launch_bounds__(256) k_prep_certs(uint32_t nsigs, uint32_t nkeys, uint32_t* sig_cert, uint32_t* counts,
                                                     uint32_t* zero4, uint32_t* status, uint32_t ncerts,
                                                     uint32_t* cert_state) {
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t i = t; i <= nsigs; i += stride) sig_cert[i] = 0u;
+    for (uint32_t i = t; i <= nsigs; i += stride) sig_cert[i] = NO_CERT;
     if (cert_state)
         for (uint32_t c = t; c < ncerts; c += stride) cert_state[c] = 0u;
     if (counts)
@@ -325,7 +327,7 @@ __global__ void __launch_bounds__(256) k_expand_count(uint32_t ncerts, uint32_t 
         const uint32_t f = cert_first[c], n = cert_n[c];
         bad = lane == 0 && (uint64_t)f + n > nsigs;
         const uint32_t end = (uint64_t)f + n > nsigs ? nsigs : f + n;   // clamped: k_cert_finalize rejects it
-        for (uint32_t v = f + lane; v < end; v += 64) sig_cert[v] = c;
+        for (uint32_t v = f + lane; v < end; v += 64) bad = (atomicExch(&sig_cert[v], c) != NO_CERT) || bad;
     }
     const uint32_t t0 = blockIdx.x * GROUP_TILE;
     if ((counts || status) && t0 < nsigs) {
@@ -495,15 +497,6 @@ hipError_t launch_group_scatter(uint32_t n, uint32_t nkeys, const uint32_t* sign
     else
         hipLaunchKernelGGL(k_scatter_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, nkeys, signer, cursor,
                            perm);
-    return hipGetLastError();
-}
-
-hipError_t launch_validate_certs(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
-                                 const uint32_t* nv, const uint32_t* signer, uint32_t* status, hipStream_t st) {
-    const uint32_t n = ncerts > nsigs ? ncerts : nsigs;
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_validate_certs, dim3(blocks_for(n, 256)), dim3(256), 0, st, ncerts, nsigs, nkeys, first, nv,
-                       signer, status);
     return hipGetLastError();
 }
 

@@ -24,6 +24,7 @@ __device__ __forceinline__ void lane_inputs(const VerifyParams& a, uint32_t i, u
     load_w8(Aw, a.keys_raw + (size_t)slot * 8);
     kinfo = in_cache ? a.key_info[slot] : 0u;
     cert = a.sig_cert[i];
+    cert = cert == NO_CERT ? 0u : cert;   // a vote outside every range: k_finish gives it no verdict
     if (MSGMODE == 0) {
         uint32_t M[8];
         load_w8(M, reinterpret_cast<const uint32_t*>(a.cert_msg) + (size_t)cert * 8);
@@ -142,7 +143,9 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
     for (uint32_t t = threadIdx.x * gridDim.x + blockIdx.x; t < cnt; t += nthr) {
         const uint32_t i = a.slow_list[t];
         uint32_t* rec = a.slow_buf + (size_t)t * SLOW_WORDS;
-        const uint32_t cert = a.sig_cert[i];
+        const uint32_t cert = a.sig_cert[i];   // slow-list entries always have an owner (k_finish)
+        const uint32_t fi = a.flags[i];
+        a.flags[i] = fi & ~NW_F_P_SAVED;       // internal bit: never returned to the caller
         if (a.cert_state[cert] & CS_DOOM) {
             rec[SLOW_KIND] = SK_SKIP;
             continue;
@@ -154,7 +157,7 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
 #endif
         ge_p3 Rp;
         if (!ge_decompress(Rp, R)) {
-            a.flags[i] |= NW_F_R_BAD;
+            a.flags[i] = (fi & ~NW_F_P_SAVED) | NW_F_R_BAD;
             atomicOr(&a.cert_state[cert], CS_DOOM);
             rec[SLOW_KIND] = SK_SKIP;
             continue;
@@ -163,7 +166,7 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
         const uint64_t tm1 = __builtin_amdgcn_s_memtime();
 #endif
         ge_p3 P;
-        if (a.flags[i] & NW_F_P_SAVED) {
+        if (fi & NW_F_P_SAVED) {
             P = load_p3(a.pslow + (size_t)i * 40);
         } else {   // y matched but x's sign did not (R = -P): recompute P
             uint32_t R2[8], S[8], h[8], slot, kinfo, c2;
@@ -182,7 +185,7 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
 #ifdef NW_SLOW_TIMING
         const uint64_t tm3 = __builtin_amdgcn_s_memtime();
         printf("slow_prep t=%u saved=%d dec=%llu P=%llu Dz8=%llu small=%d rt0=%llu rt1=%llu\n", t,
-               (a.flags[i] & NW_F_P_SAVED) ? 1 : 0, (unsigned long long)(tm1 - tm0), (unsigned long long)(tm2 - tm1),
+               (fi & NW_F_P_SAVED) ? 1 : 0, (unsigned long long)(tm1 - tm0), (unsigned long long)(tm2 - tm1),
                (unsigned long long)(tm3 - tm2), small ? 1 : 0, (unsigned long long)rt_start,
                (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
