@@ -357,6 +357,59 @@ def digest_leg(eng, dev, n_node, n_share, reps, cpu_seconds, verify_step):
     return out
 
 
+def worker_digest_leg(eng, n_batches=1250, windows=(32, 128, 1250), depth=2):
+    """The worker's Processor digests (worker/src/processor.rs:63-97) through the batched
+    asynchronous path (narwhal_amd.worker.DigestBatcher -> nw_sha512_many_async), host buffers:
+    C4's per-GPU share of 508,052-B batches arriving back to back.  Per window size: batches/s and
+    the per-batch latency from push to delivery; beside it the one-batch call and one host core
+    with hashlib (the reference's serial loop)."""
+    import hashlib
+    from narwhal_amd import worker, workload
+    host = workload.worker_batches_np(n_batches)
+    blen = host.shape[1]
+    rows = [host[i] for i in range(n_batches)]
+    out = {"batches": n_batches, "batch_bytes": blen, "depth": depth, "windows": {}}
+    for win in windows:
+        b = worker.DigestBatcher(eng, window=win, depth=depth)
+        for d, x in b.pipeline(rows[:min(2 * win, n_batches)]):   # warm the workspaces
+            pass
+        t_push = {}
+        lat = []
+        t0 = time.perf_counter()
+        for k, x in enumerate(rows):
+            t_push[id(x)] = time.perf_counter()
+            b.push(x)
+            for d, y in b.ready():
+                lat.append(time.perf_counter() - t_push[id(y)])
+        for d, y in b.drain():
+            lat.append(time.perf_counter() - t_push[id(y)])
+        dt = time.perf_counter() - t0
+        assert len(lat) == n_batches
+        lat.sort()
+        out["windows"][str(win)] = {"batches_per_s": n_batches / dt, "GBps": n_batches * blen / dt / 1e9,
+                                    "p50_latency_ms": lat[len(lat) // 2] * 1e3, "p99_latency_ms": lat[int(len(lat) * 0.99)] * 1e3,
+                                    "submissions": b.submissions}
+    last = worker.DigestBatcher(eng, window=1, depth=1)
+    one = []
+    for k in range(7):
+        t1 = time.perf_counter()
+        last.push(rows[k])
+        (d, _), = last.drain()
+        one.append(time.perf_counter() - t1)
+        assert d == hashlib.sha512(rows[k].tobytes()).digest()
+    one.sort()
+    t1 = time.perf_counter()
+    for k in range(40):
+        hashlib.sha512(rows[k].data).digest()
+    core = (time.perf_counter() - t1) / 40
+    out["one_batch_call_ms"] = {"p50": one[3] * 1e3, "min": one[0] * 1e3}
+    out["host_1core"] = {"ms_per_batch": core * 1e3, "batches_per_s": 1.0 / core, "kind": "hashlib (OpenSSL) SHA-512"}
+    out["note"] = ("latency = push -> delivery of (digest, batch) in arrival order, all batches available at once; "
+                   "a batch's digest is one chain of %d compressions, so no window delivers one sooner than the "
+                   "lone-chain time" % ((blen + 17 + 127) // 128))
+    return out
+
+
 def msm_leg(eng, n_sigs=62500, chunks=64, reps=11):
     """Keys outside the committee cache (the worker's direct verify_batch, worker/src/processor.rs:
     75-79, without loading its keys): nw_verify_batches_pk -> Pippenger MSM, host buffers."""
@@ -752,6 +805,7 @@ def main(argv=None):
         if world == 1 and c2 and not args.no_extras:
             out["host_fed"] = host_fed(eng, cs, slots, zseed)
             out["msm"] = msm_leg(eng)
+            out["worker_digest"] = worker_digest_leg(eng)
             if args.latency_samples > 0:
                 out["latency"] = latency_legs(eng, com, slots, cs, args.latency_samples)
         if world == 1 and c2 and args.digest_batches > 0:

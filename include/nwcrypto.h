@@ -196,11 +196,26 @@ int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first
 int nw_sha512(nw_ctx* ctx, const uint8_t* data, size_t len, uint8_t out[64]);
 int nw_sha512_many(nw_ctx* ctx, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                    size_t n, uint8_t (*out)[64]);
-/* Device-resident bulk digest: d_base/d_off/d_len/d_out are device pointers.  One lane per message:
- * each message is one sequential compression chain (worker batches: ~9 us per 128-B block on one
- * lane). */
+/* Device-resident bulk digest: d_base/d_off/d_len/d_out are device pointers.  Each message is one
+ * sequential compression chain: a lone 508,052-B worker batch takes ~12-15 ms whatever the number
+ * of batches in the call (up to ~1,000 chains run concurrently at that rate), DESIGN.md §5.5. */
 int nw_sha512_many_dev(nw_ctx* ctx, const uint8_t* d_base, const uint64_t* d_off,
                        const uint64_t* d_len, size_t n, uint8_t* d_out64, void* stream);
+
+/* Asynchronous many-message digest from host buffers, for a caller that keeps receiving work while
+ * the GPU hashes (the worker's Processor loop, worker/src/processor.rs:63-97, replacing one
+ * serial Sha512::digest per batch at :65 by one submission per window of batches).  Message i is
+ * msg[i] (len[i] bytes); the buffers must stay valid until nw_job_wait returns (the worker keeps
+ * each batch until it is stored under its digest anyway).  The call enqueues the upload, the
+ * digest kernel and the download and returns a job at once.
+ *   nw_job_done(job): 1 when the digests are ready, 0 while in flight, < 0 on a device error.
+ *   nw_job_wait(job): blocks until out (n x 64 bytes) holds the digests, then frees the job; every
+ *                     job must be waited for exactly once, before nw_ctx_destroy. */
+typedef struct nw_job nw_job;
+int nw_sha512_many_async(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, size_t n,
+                         uint8_t (*out)[64], nw_job** job);
+int nw_job_done(nw_job* job);
+int nw_job_wait(nw_job* job);
 
 /* ---- signing (crypto::Signature::new / generate_keypair, crypto/src/lib.rs:163-191) -------------
  * Low-volume in the reference; here it makes synthetic workloads.  RFC 8032 Ed25519 over

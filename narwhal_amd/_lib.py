@@ -59,7 +59,8 @@ DAG_NOT_CERTIFICATE = 8
 ABI_VERSION = 2    # NW_ABI_VERSION of include/nwcrypto.h this binding is written against
 
 _OPTIONAL = {"nw_abi_version", "nw_profile_read_sigs", "nw_base_window", "nw_cert_batch_decode", "nw_cert_batch_size",
-             "nw_cert_batch_view", "nw_cert_batch_free", "nw_cert_batch_verify", "nw_certificates_verify"}
+             "nw_cert_batch_view", "nw_cert_batch_free", "nw_cert_batch_verify", "nw_certificates_verify",
+             "nw_sha512_many_async", "nw_job_done", "nw_job_wait"}
 
 
 def _load() -> ctypes.CDLL:
@@ -88,6 +89,9 @@ def _load() -> ctypes.CDLL:
         "nw_sha512": (I, [P, P, S, P]),
         "nw_sha512_many": (I, [P, P, P, P, S, P]),
         "nw_sha512_many_dev": (I, [P, P, P, P, S, P, P]),
+        "nw_sha512_many_async": (I, [P, P, P, S, P, ctypes.POINTER(P)]),
+        "nw_job_done": (I, [P]),
+        "nw_job_wait": (I, [P]),
         "nw_sign_many": (I, [P, P, P, S, S, P, P]),
         "nw_sign_many_dev": (I, [P, P, P, S, S, P, P, P]),
         "nw_profile_enable": (I, [P, I]),
@@ -463,6 +467,11 @@ class Engine:
                    "nw_profile_read_sigs")
         return ms.value, n.value, sigs.value
 
+    def sha512_many_submit(self, messages) -> "DigestJob":
+        """nw_sha512_many_async: enqueue the digests of ``messages`` (bytes-like objects or uint8
+        numpy arrays, kept referenced until the job is waited for) and return at once."""
+        return DigestJob(self, messages)
+
     def sha512_many_dev(self, d_base, d_off, d_len, n, d_out, stream):
         self.check(LIB.nw_sha512_many_dev(self._ctx, d_base, d_off, d_len, n, d_out, stream), "nw_sha512_many_dev")
 
@@ -475,6 +484,47 @@ class Engine:
         self.check(LIB.nw_cert_batch_verify(self._ctx, batch.handle, _buf(bytes(zseed)), cert_base, out),
                    "nw_cert_batch_verify")
         return list(out[:n])
+
+
+class DigestJob:
+    """One nw_sha512_many_async submission in flight.  ``done()`` polls; ``wait()`` returns the
+    64-byte digests in submission order (exactly once).  The message buffers stay referenced by
+    the job until then, as the ABI requires."""
+
+    def __init__(self, engine: Engine, messages):
+        import numpy as np
+        self._engine = engine
+        self._msgs = [m if isinstance(m, np.ndarray) else np.frombuffer(m, np.uint8) for m in messages]
+        n = len(self._msgs)
+        self.n = n
+        self._ptrs = np.array([m.ctypes.data if m.size else 0 for m in self._msgs], np.uint64)
+        self._lens = np.array([m.size for m in self._msgs], np.uint64)
+        self._out = np.zeros((max(n, 1), 64), np.uint8)
+        self._job = ctypes.c_void_p()
+        engine.check(LIB.nw_sha512_many_async(engine.handle, self._ptrs.ctypes.data, self._lens.ctypes.data, n,
+                                              self._out.ctypes.data, ctypes.byref(self._job)), "nw_sha512_many_async")
+
+    def done(self) -> bool:
+        if not self._job:
+            return True
+        rc = LIB.nw_job_done(self._job)
+        if rc < 0 or rc > 1:
+            raise DeviceError("nw_job_done failed (rc=%d)" % rc)
+        return rc == 1
+
+    def wait(self) -> list:
+        if self._job:
+            job, self._job = self._job, ctypes.c_void_p()
+            self._engine.check(LIB.nw_job_wait(job), "nw_job_wait")
+            self._msgs = None
+        return [bytes(self._out[i]) for i in range(self.n)]
+
+    def __del__(self):
+        try:
+            if self._job:
+                LIB.nw_job_wait(self._job)   # a job must be waited for exactly once
+        except Exception:
+            pass
 
 
 class CommitteeABI:

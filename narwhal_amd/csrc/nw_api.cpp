@@ -276,6 +276,19 @@ private:
     bool sync_on_release_ = false;
 };
 
+}  // namespace
+
+// An asynchronous host-buffer call in flight (nw_sha512_many_async): its workspace lease, the
+// caller's output and where the digests land in the workspace's pinned buffer.
+struct nw_job {
+    std::unique_ptr<Lease> lease;
+    uint8_t* out = nullptr;
+    size_t n = 0;
+    size_t o_out = 0;
+};
+
+namespace {
+
 // Wait for every call that may still read the key tables (exclusive key lock held).  Every lease
 // is taken under the shared key lock, so no lease is live here and nothing else touches
 // pending/done while we read them.
@@ -1477,6 +1490,100 @@ int nw_sha512(nw_ctx* ctx, const uint8_t* data, size_t len, uint8_t out[64]) {
     const uint64_t off = 0, ln = len;
     static const uint8_t empty[1] = {0};
     return nw_sha512_many(ctx, data ? data : empty, &off, &ln, 1, reinterpret_cast<uint8_t(*)[64]>(out));
+}
+
+// Asynchronous batch digest (the worker's Processor loop, worker/src/processor.rs:63-97).  The job
+// owns a workspace lease from submit to wait, so its pinned staging buffer (small messages in, the
+// digests out) is never reused under it; it does not mark the workspace pending and holds no key
+// lock (a digest reads no key table, so committee loads need not wait for it).  Device layout:
+// the staged small messages first (one DMA), then the large ones copied straight from the caller's
+// buffers (from 64 KiB: a worker batch is ~500 KB and the pageable H2D runs at the pinned rate,
+// where a staging memcpy would add host work per byte), every message at a 16-byte aligned offset.
+constexpr size_t kAsyncDirectBytes = 64u << 10;
+int nw_sha512_many_async(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, size_t n, uint8_t (*out)[64],
+                         nw_job** job) {
+    if (!ctx || !job || (n && (!msg || !len || !out))) return NW_ERR_ARG;
+    *job = nullptr;
+    if (n > 0xFFFFFFF0u) return NW_ERR_ARG;
+    for (size_t i = 0; i < n; ++i)
+        if (len[i] && !msg[i]) return NW_ERR_ARG;
+    auto j = std::make_unique<nw_job>();
+    j->out = reinterpret_cast<uint8_t*>(out);
+    j->n = n;
+    if (n == 0) {
+        *job = j.release();
+        return NW_OK;
+    }
+    NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    auto align16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
+    std::vector<uint64_t> off(n);
+    size_t small_bytes = 0, total = 0;
+    for (size_t i = 0; i < n; ++i)
+        if (len[i] < kAsyncDirectBytes) {
+            off[i] = small_bytes;
+            small_bytes += align16(len[i]);
+        }
+    total = small_bytes;
+    for (size_t i = 0; i < n; ++i)
+        if (len[i] >= kAsyncDirectBytes) {
+            off[i] = total;
+            total += align16(len[i]);
+        }
+    j->lease = std::make_unique<Lease>(ctx);
+    Workspace* ws = j->lease->ws();
+    if (!ws) return NW_ERR_DEVICE;
+    hipStream_t st = ws->stream;
+    NW_TRY(j->lease->bind(st, true), "hipStreamWaitEvent");
+    const size_t o_small = 0, o_off = align256(small_bytes), o_len = o_off + align256(n * 8),
+                 o_out = o_len + align256(n * 8);
+    j->o_out = o_out;
+    NW_TRY(ws->h_io.ensure(o_out + n * 64), "pinned io");
+    NW_TRY(ws->ensure(ws->w_msg, total + 16), "ws msg");
+    NW_TRY(ws->ensure(ws->w_msg_off, n * 8), "ws off");
+    NW_TRY(ws->ensure(ws->w_msg_len, n * 8), "ws len");
+    NW_TRY(ws->ensure(ws->w_out, n * 64), "ws out");
+    uint8_t* h = ws->h_io.bytes();
+    for (size_t i = 0; i < n; ++i)
+        if (len[i] < kAsyncDirectBytes && len[i]) std::memcpy(h + o_small + off[i], msg[i], len[i]);
+    std::memcpy(h + o_off, off.data(), n * 8);
+    for (size_t i = 0; i < n; ++i) reinterpret_cast<uint64_t*>(h + o_len)[i] = len[i];
+    uint8_t* d_msg = ws->w_msg.as<uint8_t>();
+    if (small_bytes) NW_TRY(hipMemcpyAsync(d_msg, h + o_small, small_bytes, hipMemcpyHostToDevice, st), "H2D small");
+    NW_TRY(hipMemcpyAsync(ws->w_msg_off.p, h + o_off, n * 8, hipMemcpyHostToDevice, st), "H2D off");
+    NW_TRY(hipMemcpyAsync(ws->w_msg_len.p, h + o_len, n * 8, hipMemcpyHostToDevice, st), "H2D len");
+    for (size_t i = 0; i < n; ++i)
+        if (len[i] >= kAsyncDirectBytes)
+            NW_TRY(hipMemcpyAsync(d_msg + off[i], msg[i], len[i], hipMemcpyHostToDevice, st), "H2D message");
+    NW_TRY(launch_sha512_many((uint32_t)n, d_msg, ws->w_msg_off.as<uint64_t>(), ws->w_msg_len.as<uint64_t>(),
+                              ws->w_out.as<uint8_t>(), st),
+           "k_sha512_many");
+    NW_TRY(hipMemcpyAsync(h + o_out, ws->w_out.p, n * 64, hipMemcpyDeviceToHost, st), "D2H digests");
+    NW_TRY(hipEventRecord(ws->done, st), "hipEventRecord");
+    *job = j.release();
+    return NW_OK;
+}
+
+int nw_job_done(nw_job* job) {
+    if (!job) return NW_ERR_ARG;
+    if (!job->lease) return 1;
+    const hipError_t e = hipEventQuery(job->lease->ws()->done);
+    if (e == hipSuccess) return 1;
+    return e == hipErrorNotReady ? 0 : -NW_ERR_DEVICE;
+}
+
+int nw_job_wait(nw_job* job) {
+    if (!job) return NW_ERR_ARG;
+    std::unique_ptr<nw_job> own(job);
+    if (!own->lease) return NW_OK;
+    Workspace* ws = own->lease->ws();
+    const hipError_t e = hipEventSynchronize(ws->done);
+    if (e != hipSuccess) {
+        tl_last_error = std::string("nw_job_wait: ") + hipGetErrorString(e);
+        return NW_ERR_DEVICE;   // the lease synchronizes its stream on release
+    }
+    std::memcpy(own->out, ws->h_io.bytes() + own->o_out, own->n * 64);
+    own->lease->synced();
+    return NW_OK;
 }
 
 int nw_sign_many_dev(nw_ctx* ctx, const uint8_t* d_seed32, const uint8_t* d_msgs, size_t msg_len, size_t n,

@@ -36,7 +36,9 @@ NW_HD uint64_t rotr64v(uint64_t x, uint32_t n) {   // 0 < n < 32, per lane
 #endif
 }
 
-// value of the partner lane (lane ^ 1); device only
+// value of the partner lane (lane ^ 1); device only.  (Reading it through the add itself,
+// v_add_co/v_addc_co _dpp, saves the two moves but leaves the bitop3 results without the
+// independent instructions that cover their wait states: the compiler then pads with s_nop.)
 __device__ __forceinline__ uint64_t swap_pair64(uint64_t x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, 0xB1, 0xF, 0xF, false);
@@ -70,30 +72,41 @@ struct Sha2L {
         return s + (f + (z + swap_pair64(B)));
     }
 
+    // K_t + W_t is read KW_AHEAD steps before its use into a register ring: a read issued in the
+    // step that consumes it exposes the whole LDS latency (~50-120 cycles on a 20-instruction step)
+    // to the chain once per round.
+    static constexpr int KW_AHEAD = 4;
+
     // step T of a block on the register array x (the roles rotate with period 4; T is a
     // compile-time constant so every index below is a fixed register)
     template <int T, class KW>
-    __device__ __forceinline__ void block_step(uint64_t x[4], const uint64_t h[4], KW& kw) const {
+    __device__ __forceinline__ void block_step(uint64_t x[4], const uint64_t h[4], uint64_t q[KW_AHEAD], KW& kw) const {
         uint64_t& D = x[(7 - T) & 3];
-        // steps 80, 81: the even lane's result is discarded, the odd lane's kw must still be 1
-        uint64_t nv = step(x[(4 - T) & 3], x[(5 - T) & 3], x[(6 - T) & 3], D, kw(T < 80 ? T : 79));
+        // steps 80, 81: the even lane's result is discarded, the odd lane's kw must still be 1:
+        // they reuse K_79 + W_79's slot, which is never refilled
+        const uint64_t k = q[(T < 80 ? T : 79) % KW_AHEAD];
+        if constexpr (T + KW_AHEAD < 80) q[T % KW_AHEAD] = kw(T + KW_AHEAD);
+        uint64_t nv = step(x[(4 - T) & 3], x[(5 - T) & 3], x[(6 - T) & 3], D, k);
         if (T == 0) nv = sel64(m, h[1], nv);           // odd: a_{-1} = b
         else if (T == 1) nv = sel64(m, h[0], nv);      // odd: a_0 = a
         else if (T >= 80) nv = sel64(m, nv, D);        // even: keep e..h
         D = nv;
-        if constexpr (T + 1 < 82) block_step<T + 1>(x, h, kw);
+        if constexpr (T + 1 < 82) block_step<T + 1>(x, h, q, kw);
     }
 
     // One compression.  h = this lane's half of the chaining state (even: e f g h, odd: a b c d);
     // kw(t) = K_t + W_t on the even lane and 1 on the odd lane, t = 0..79.
     template <class KW>
     __device__ __forceinline__ void block(uint64_t h[4], KW kw) const {
+        uint64_t q[KW_AHEAD];
+#pragma unroll
+        for (int t = 0; t < KW_AHEAD; ++t) q[t] = kw(t);
         uint64_t x[4];
         x[0] = sel64(m, h[2], h[0]);   // newest: e (even) / a_{-2} = c (odd)
         x[1] = sel64(m, h[3], h[1]);   // f / a_{-3} = d
         x[2] = h[2];                   // g / (unused)
         x[3] = h[3];                   // h / (unused)
-        block_step<0>(x, h, kw);
+        block_step<0>(x, h, q, kw);
         // even: (e f g h) = x[0] x[1] x[2] x[3];  odd: (a b c d) = x[2] x[3] x[0] x[1]
         h[0] += sel64(m, x[2], x[0]);
         h[1] += sel64(m, x[3], x[1]);
