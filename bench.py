@@ -84,6 +84,20 @@ def traffic_per_launch():
         return json.load(f).get("hbm_bytes_per_launch")
 
 
+def clock_frac_profile():
+    """k_verify's fraction of the MAD peak per shader cycle (both kernels timed in cycles by PMC
+    GRBM_GUI_ACTIVE: tools/r04_pmc.sh + tools/clock_frac.py -> profiles/r04/clock_frac_r04h.json)."""
+    path = os.path.join(ROOT, "profiles", "r04", "clock_frac_r04h.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return {"frac_per_cycle": d["frac_per_cycle"], "peak_mad_per_cycle": d["peak_mad_per_cycle"],
+            "kverify_alg_mad_per_cycle": d["kverify_alg_mad_per_cycle"],
+            "source": "profiles/r04/clock_frac_r04h.json (PMC GRBM_GUI_ACTIVE on tools/valu_peak and on k_verify "
+                      "at C2, same 162-FM work model)"}
+
+
 def host_cores():
     """Host threads this process may run on (the whole host unless the scheduler restricts it)."""
     return len(os.sched_getaffinity(0))
@@ -123,8 +137,8 @@ def cpu_thread_candidates():
 
 
 def cpu_baseline(cs, com, seconds, probe_seconds=2.5, label="C2"):
-    """Oracle restatement timed on the host cores (rank 0, N = 1 only): bounded sample of
-    certificates.  A short sweep over the candidate thread counts (cpu_thread_candidates; forced
+    """Oracle restatement timed on the host cores (rank 0, at every world size, after the timed
+    region): bounded sample of certificates.  A short sweep over the candidate thread counts (cpu_thread_candidates; forced
     with NW_CPU_THREADS) picks the host's best rate, which is then timed on the main sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import nw_ref   # C restatement of dalek's u64 backend (oracle/nw_ref.c); test/baseline only
@@ -165,7 +179,8 @@ def cpu_baseline(cs, com, seconds, probe_seconds=2.5, label="C2"):
             "thread_sweep_sigs_per_s": sweep or None,
             "sample": "%d certificates x %d votes of the %s workload (%d sigs) in %.1f s on %d threads (best of the "
                       "sweep); oracle/nw_ref.c (C restatement of ed25519-dalek 1.0.1 u64 backend: per-vote A "
-                      "decompression + Straus MSM, as crypto/src/lib.rs:206-219)"
+                      "decompression + Straus MSM below 190 votes, Pippenger above, as dalek's verify_batch via "
+                      "crypto/src/lib.rs:206-219)"
                       % (done_certs, int(cs.cert_n[0]), label, done_sigs, dt, threads)}
 
 
@@ -222,20 +237,31 @@ def host_fed(eng, cs, slots, zseed, chunks=8, threads=4, reps=5):
         ok, _, _ = eng.verify_certs_np(p[0], p[1], p[2], p[3], p[4], zseed, p[5])
         return bool(ok.all())
 
+    def fresh(ps):   # new host buffers, as a node's network receives would hand over
+        return [(a, b, c.copy(), d.copy(), e.copy(), f) for a, b, c, d, e, f in ps]
+
+    fresh_sets = [fresh(parts) for _ in range(reps)]
     with ThreadPoolExecutor(threads) as ex:
         assert all(ex.map(run, parts))   # warm every workspace
-        ts = []
-        for _ in range(reps):
+        ts, tf = [], []
+        for r in range(reps):
             t0 = time.perf_counter()
             ok = all(ex.map(run, parts))
             ts.append(time.perf_counter() - t0)
             assert ok
+            t0 = time.perf_counter()
+            ok = all(ex.map(run, fresh_sets[r]))
+            tf.append(time.perf_counter() - t0)
+            assert ok
     ts.sort()
+    tf.sort()
     dt = ts[len(ts) // 2]
     return {"value": cs.nsigs / dt, "unit": "sigs/s", "ms": dt * 1e3, "ms_reps": [t * 1e3 for t in ts],
-            "note": "nw_verify_certs on pageable host buffers (signature arrays copied H2D directly, the rest "
-                    "staged), %d calls on %d threads, median of %d passes; PCIe and host packing included"
-                    % (chunks, threads, reps)}
+            "fresh_buffers": {"value": cs.nsigs / tf[len(tf) // 2], "ms": tf[len(tf) // 2] * 1e3,
+                              "ms_reps": [t * 1e3 for t in tf]},
+            "note": "nw_verify_certs on pageable host buffers (every input staged through the call's pinned "
+                    "buffer), %d calls on %d threads, median of %d passes; PCIe and host packing included; "
+                    "fresh_buffers: each pass on newly allocated host arrays" % (chunks, threads, reps)}
 
 
 def digest_leg(eng, dev, n_node, n_share, reps, cpu_seconds, verify_step):
@@ -755,6 +781,7 @@ def main(argv=None):
             "bound": "valu", "kernel": "k_verify", "achieved": achieved, "peak": peak, "unit": "TMAD/s",
             "frac": achieved / peak,
             "traffic": traffic_per_launch() if args.config == "C2" else None,
+            "per_cycle": clock_frac_profile() if args.config == "C2" else None,
             "avg_launch_ms": avg_launch_s * 1e3, "launches": kn,
             "work_model": "%.0f sigs/launch (%d launches per step) x %d FM/sig (7 FM per mixed addition x (%d basepoint "
                           "+ %d key - 1) comb positions + 1 FM for the chain's first entry, key window %d) x 100 u32 "

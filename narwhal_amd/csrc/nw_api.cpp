@@ -491,7 +491,7 @@ struct PreStaged {
     uint32_t* zero4;        // [4]
     uint32_t* cert_state;   // [ncerts]
 };
-// Calls below this many signatures (and whose staged bytes fit kDirectCopyBytes) use PreStaged:
+// Calls below this many signatures (and whose staged bytes fit kSmallCallBytes) use PreStaged:
 // the signer grouping (k_expand_count's histogram) only runs from kGroupMinSigs up.
 constexpr size_t kStagedMaxSigs = 16384;
 static_assert(kStagedMaxSigs <= kGroupMinSigs, "staged calls never group");
@@ -681,17 +681,20 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
 // Host-buffer inputs of one call: segments are packed into the workspace's pinned buffer (256-B
 // aligned) and copied to their device buffers with asynchronous DMAs, so a call issues no
 // pageable copies and no intermediate synchronization (the call's final stream sync releases the
-// buffer).  Segments of at least kDirectCopyBytes are copied from the caller's buffer directly:
-// the runtime's pageable H2D runs at the pinned rate (56 GB/s on MI355X) while a memcpy into the
-// staging buffer adds serial host work at 34 GB/s (tools/host_fed_probe.py).
-constexpr size_t kDirectCopyBytes = 2u << 20;
+// buffer).  Every segment is staged, large ones included: the runtime's pageable H2D runs at the
+// pinned rate only for host pages it has already seen; the first copy from a fresh buffer pins its
+// pages and took 7-10 ms per 8 MB on MI355X (profiles/r04/host_fed_trace_r04h.txt), and a node's
+// input buffers are fresh on every call (network receives).  The staging memcpy costs ~0.3 ms per
+// 8 MB at 31-34 GB/s (tools/host_fed_probe.py).
+// Calls whose whole input fits this many bytes take the one-DMA small-call path.
+constexpr size_t kSmallCallBytes = 2u << 20;
 
 class Stager {
 public:
     Stager(Workspace* ws, hipStream_t st) : ws_(ws), st_(st) {}
     // upper bound of the staged bytes of the call (one allocation, before any segment)
     hipError_t reserve(size_t bytes) { return ws_->h_io.ensure(bytes + 16 * 256); }
-    static size_t room(size_t bytes) { return bytes >= kDirectCopyBytes ? 0 : align256(bytes); }
+    static size_t room(size_t bytes) { return align256(bytes); }
     uint8_t* alloc(size_t n) {
         uint8_t* h = ws_->h_io.bytes() + off_;
         off_ = align256(off_ + n);
@@ -702,7 +705,6 @@ public:
     }
     hipError_t put(void* dst, const void* src, size_t n) {
         if (!n) return hipSuccess;
-        if (n >= kDirectCopyBytes) return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, st_);
         uint8_t* h = alloc(n);
         std::memcpy(h, src, n);
         return copy(dst, h, n);
@@ -713,6 +715,19 @@ private:
     hipStream_t st_;
     size_t off_ = 0;
 };
+
+// Upload n bytes of host memory through pinned staging at h: 4 MiB chunks, each chunk's DMA issued
+// as soon as it is staged, so the DMA of one chunk overlaps the memcpy of the next.
+constexpr size_t kStageChunk = 4u << 20;
+hipError_t staged_h2d(uint8_t* h, uint8_t* dst, const uint8_t* src, size_t n, hipStream_t st) {
+    for (size_t c = 0; c < n; c += kStageChunk) {
+        const size_t m = n - c < kStageChunk ? n - c : kStageChunk;
+        std::memcpy(h + c, src + c, m);
+        const hipError_t e = hipMemcpyAsync(dst + c, h + c, m, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
 
 size_t message_bytes(const size_t* len, size_t n) {
     size_t total = 0;
@@ -926,7 +941,7 @@ int run_generic(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const
             rc = enqueue_strict_var(ctx, ws, n, st, ws->w_ok.as<uint8_t>());
             if (rc != NW_OK) return rc;
         }
-    } else if (n <= kStagedMaxSigs && packed_bytes(message_bytes(len, n), n) < kDirectCopyBytes) {
+    } else if (n <= kStagedMaxSigs && packed_bytes(message_bytes(len, n), n) < kSmallCallBytes) {
         // one-message paths (Signature::verify, one certificate's verify_batch): every input and the
         // preamble state in ONE staged H2D, no preamble kernels, both outputs in ONE D2H
         const size_t total = message_bytes(len, n);
@@ -1293,11 +1308,10 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
     if (!ws) return NW_ERR_DEVICE;
     hipStream_t st = ws->stream;
     NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
-    // Small calls (single-certificate latency): every input staged into pinned memory, one H2D and
-    // one D2H.  Large calls: the signature and signer arrays go straight from the caller's pageable
-    // buffers (see kDirectCopyBytes).
-    const bool direct = nsigs * 64 >= kDirectCopyBytes;
-    const bool staged = !direct && nsigs <= kStagedMaxSigs;   // preamble state rides along: no preamble kernels
+    // Every input is staged into pinned memory (see kSmallCallBytes): one D2H for the outputs; small
+    // calls also carry the preamble state and go up in one H2D.  The signature array of a large call
+    // goes up in 4 MiB chunks, each DMA overlapping the staging memcpy of the next chunk.
+    const bool staged = nsigs <= kStagedMaxSigs;   // preamble state rides along: no preamble kernels
     const size_t o_sig = 0, o_signer = align256(o_sig + nsigs * 64), o_first = align256(o_signer + nsigs * 4),
                  o_nv = align256(o_first + ncerts * 4), o_msg = align256(o_nv + ncerts * 4),
                  o_pre = align256(o_msg + ncerts * 32),
@@ -1309,22 +1323,20 @@ int nw_verify_certs(nw_ctx* ctx, const nw_cert* certs, size_t ncerts, const uint
     uint8_t* h = ws->h_io.bytes();
     uint8_t* d_in = ws->w_io.as<uint8_t>();
     uint8_t* d_out = d_in + in_bytes;
-    if (nsigs && !direct) {
-        std::memcpy(h + o_sig, sig, nsigs * 64);
-        std::memcpy(h + o_signer, signer_slot, nsigs * 4);
-    }
+    if (nsigs) std::memcpy(h + o_signer, signer_slot, nsigs * 4);
     std::memcpy(h + o_first, first.data(), ncerts * 4);
     std::memcpy(h + o_nv, nv.data(), ncerts * 4);
     std::memcpy(h + o_msg, msg, ncerts * 32);
     PreStaged pre{};
     if (staged) prestage(h + o_pre, d_in + o_pre, first.data(), nv.data(), ncerts, nsigs, pre);
-    if (direct) {
-        NW_TRY(hipMemcpyAsync(d_in + o_sig, sig, nsigs * 64, hipMemcpyHostToDevice, st), "H2D sig");
-        NW_TRY(hipMemcpyAsync(d_in + o_signer, signer_slot, nsigs * 4, hipMemcpyHostToDevice, st), "H2D signer");
-        NW_TRY(hipMemcpyAsync(d_in + o_first, h + o_first, in_bytes - o_first, hipMemcpyHostToDevice, st),
-               "H2D inputs");
-    } else {
+    const size_t sig_bytes = nsigs * 64;
+    if (sig_bytes < kStageChunk) {
+        if (sig_bytes) std::memcpy(h + o_sig, sig, sig_bytes);
         NW_TRY(hipMemcpyAsync(d_in, h, in_bytes, hipMemcpyHostToDevice, st), "H2D inputs");
+    } else {
+        NW_TRY(hipMemcpyAsync(d_in + o_signer, h + o_signer, in_bytes - o_signer, hipMemcpyHostToDevice, st),
+               "H2D inputs");
+        NW_TRY(staged_h2d(h + o_sig, d_in + o_sig, reinterpret_cast<const uint8_t*>(sig), sig_bytes, st), "H2D sig");
     }
     int rc = enqueue_certs(ctx, ws, ncerts, reinterpret_cast<const uint32_t*>(d_in + o_first),
                            reinterpret_cast<const uint32_t*>(d_in + o_nv), nsigs, d_in + o_sig,
@@ -1474,15 +1486,23 @@ int nw_sha512_many(nw_ctx* ctx, const uint8_t* base, const uint64_t* off, const 
     NW_TRY(ws->ensure(ws->w_msg_off, n * 8), "ws off");
     NW_TRY(ws->ensure(ws->w_msg_len, n * 8), "ws len");
     NW_TRY(ws->ensure(ws->w_out, n * 64), "ws out");
-    if (span) NW_TRY(hipMemcpyAsync(ws->w_msg.p, base + lo, span, hipMemcpyHostToDevice, st), "H2D data");
-    NW_TRY(hipMemcpyAsync(ws->w_msg_off.p, roff.data(), n * 8, hipMemcpyHostToDevice, st), "H2D off");
-    NW_TRY(hipMemcpyAsync(ws->w_msg_len.p, len, n * 8, hipMemcpyHostToDevice, st), "H2D len");
+    // everything through the pinned buffer (see kSmallCallBytes): offsets, lengths, then the data
+    const size_t o_off = 0, o_len = align256(n * 8), o_data = o_len + align256(n * 8);
+    NW_TRY(ws->h_io.ensure(std::max(o_data + span, n * 64)), "pinned io");
+    uint8_t* h = ws->h_io.bytes();
+    std::memcpy(h + o_off, roff.data(), n * 8);
+    std::memcpy(h + o_len, len, n * 8);
+    NW_TRY(hipMemcpyAsync(ws->w_msg_off.p, h + o_off, n * 8, hipMemcpyHostToDevice, st), "H2D off");
+    NW_TRY(hipMemcpyAsync(ws->w_msg_len.p, h + o_len, n * 8, hipMemcpyHostToDevice, st), "H2D len");
+    if (span) NW_TRY(staged_h2d(h + o_data, ws->w_msg.as<uint8_t>(), base + lo, span, st), "H2D data");
     NW_TRY(launch_sha512_many((uint32_t)n, ws->w_msg.as<uint8_t>(), ws->w_msg_off.as<uint64_t>(),
                               ws->w_msg_len.as<uint64_t>(), ws->w_out.as<uint8_t>(), st),
            "k_sha512_many");
-    NW_TRY(hipMemcpyAsync(out, ws->w_out.p, n * 64, hipMemcpyDeviceToHost, st), "D2H digests");
+    // the uploads have completed in stream order before this copy reuses the pinned buffer
+    NW_TRY(hipMemcpyAsync(h, ws->w_out.p, n * 64, hipMemcpyDeviceToHost, st), "D2H digests");
     NW_TRY(hipStreamSynchronize(st), "sync");
     lease.synced();
+    std::memcpy(out, h, n * 64);
     return NW_OK;
 }
 
@@ -1493,13 +1513,12 @@ int nw_sha512(nw_ctx* ctx, const uint8_t* data, size_t len, uint8_t out[64]) {
 }
 
 // Asynchronous batch digest (the worker's Processor loop, worker/src/processor.rs:63-97).  The job
-// owns a workspace lease from submit to wait, so its pinned staging buffer (small messages in, the
+// owns a workspace lease from submit to wait, so its pinned staging buffer (the messages in, the
 // digests out) is never reused under it; it does not mark the workspace pending and holds no key
-// lock (a digest reads no key table, so committee loads need not wait for it).  Device layout:
-// the staged small messages first (one DMA), then the large ones copied straight from the caller's
-// buffers (from 64 KiB: a worker batch is ~500 KB and the pageable H2D runs at the pinned rate,
-// where a staging memcpy would add host work per byte), every message at a 16-byte aligned offset.
-constexpr size_t kAsyncDirectBytes = 64u << 10;
+// lock (a digest reads no key table, so committee loads need not wait for it).  The messages are
+// packed into the pinned buffer at 16-byte aligned offsets (a worker's batches are fresh buffers
+// on every call: see kSmallCallBytes for why nothing is copied from pageable memory), and every
+// 4 MiB packed is sent at once, so the DMAs overlap the packing.
 int nw_sha512_many_async(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, size_t n, uint8_t (*out)[64],
                          nw_job** job) {
     if (!ctx || !job || (n && (!msg || !len || !out))) return NW_ERR_ARG;
@@ -1515,27 +1534,18 @@ int nw_sha512_many_async(nw_ctx* ctx, const uint8_t* const* msg, const size_t* l
         return NW_OK;
     }
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
-    auto align16 = [](size_t x) { return (x + 15) & ~(size_t)15; };
     std::vector<uint64_t> off(n);
-    size_t small_bytes = 0, total = 0;
-    for (size_t i = 0; i < n; ++i)
-        if (len[i] < kAsyncDirectBytes) {
-            off[i] = small_bytes;
-            small_bytes += align16(len[i]);
-        }
-    total = small_bytes;
-    for (size_t i = 0; i < n; ++i)
-        if (len[i] >= kAsyncDirectBytes) {
-            off[i] = total;
-            total += align16(len[i]);
-        }
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        off[i] = total;
+        total += (len[i] + 15) & ~(size_t)15;
+    }
     j->lease = std::make_unique<Lease>(ctx);
     Workspace* ws = j->lease->ws();
     if (!ws) return NW_ERR_DEVICE;
     hipStream_t st = ws->stream;
     NW_TRY(j->lease->bind(st, true), "hipStreamWaitEvent");
-    const size_t o_small = 0, o_off = align256(small_bytes), o_len = o_off + align256(n * 8),
-                 o_out = o_len + align256(n * 8);
+    const size_t o_off = 0, o_len = align256(n * 8), o_msg = o_len + align256(n * 8), o_out = o_msg + align256(total);
     j->o_out = o_out;
     NW_TRY(ws->h_io.ensure(o_out + n * 64), "pinned io");
     NW_TRY(ws->ensure(ws->w_msg, total + 16), "ws msg");
@@ -1543,17 +1553,21 @@ int nw_sha512_many_async(nw_ctx* ctx, const uint8_t* const* msg, const size_t* l
     NW_TRY(ws->ensure(ws->w_msg_len, n * 8), "ws len");
     NW_TRY(ws->ensure(ws->w_out, n * 64), "ws out");
     uint8_t* h = ws->h_io.bytes();
-    for (size_t i = 0; i < n; ++i)
-        if (len[i] < kAsyncDirectBytes && len[i]) std::memcpy(h + o_small + off[i], msg[i], len[i]);
     std::memcpy(h + o_off, off.data(), n * 8);
     for (size_t i = 0; i < n; ++i) reinterpret_cast<uint64_t*>(h + o_len)[i] = len[i];
-    uint8_t* d_msg = ws->w_msg.as<uint8_t>();
-    if (small_bytes) NW_TRY(hipMemcpyAsync(d_msg, h + o_small, small_bytes, hipMemcpyHostToDevice, st), "H2D small");
     NW_TRY(hipMemcpyAsync(ws->w_msg_off.p, h + o_off, n * 8, hipMemcpyHostToDevice, st), "H2D off");
     NW_TRY(hipMemcpyAsync(ws->w_msg_len.p, h + o_len, n * 8, hipMemcpyHostToDevice, st), "H2D len");
-    for (size_t i = 0; i < n; ++i)
-        if (len[i] >= kAsyncDirectBytes)
-            NW_TRY(hipMemcpyAsync(d_msg + off[i], msg[i], len[i], hipMemcpyHostToDevice, st), "H2D message");
+    uint8_t* d_msg = ws->w_msg.as<uint8_t>();
+    size_t sent = 0;
+    for (size_t i = 0; i < n; ++i) {
+        if (len[i]) std::memcpy(h + o_msg + off[i], msg[i], len[i]);
+        const size_t packed = i + 1 < n ? off[i + 1] : total;
+        if (packed - sent >= kStageChunk || (i + 1 == n && packed > sent)) {
+            NW_TRY(hipMemcpyAsync(d_msg + sent, h + o_msg + sent, packed - sent, hipMemcpyHostToDevice, st),
+                   "H2D messages");
+            sent = packed;
+        }
+    }
     NW_TRY(launch_sha512_many((uint32_t)n, d_msg, ws->w_msg_off.as<uint64_t>(), ws->w_msg_len.as<uint64_t>(),
                               ws->w_out.as<uint8_t>(), st),
            "k_sha512_many");

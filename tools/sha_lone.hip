@@ -159,7 +159,8 @@ static void host_rounds(uint32_t nb, const uint64_t* kw, uint64_t st[8]) {
 // Variants of k_sha512_split2 (same code, stamps added) to find what couples the round wave to
 // its placement.  MODE 0: as shipped; 1: the round wave reads K+W from a private LDS copy filled
 // once (the schedule waves still run and write kw); 2: the schedule waves use synthetic block
-// words instead of global loads; 3: the schedule waves skip their work (barriers only).
+// words instead of global loads; 3: the schedule waves skip their work (barriers only); 4 / 5: as
+// 0 / 3 with 70 KB of extra LDS, so no second workgroup fits on the CU (LDS placement test).
 // rec[0] round-wave cycles, rec[1] its 100 MHz ticks, rec[2] round-wave barrier cycles,
 // rec[3] schedule wave A busy cycles (barrier exit -> next arrival), rec[4..6] HW_ID of the waves.
 template <int MODE>
@@ -167,11 +168,16 @@ __global__ void __launch_bounds__(192) k_split2_x(uint32_t n, const uint8_t* bas
                                                   const uint64_t* len, uint64_t* rec) {
     __shared__ uint64_t kw[3][80][SPLIT2_COLS];
     __shared__ uint64_t kfix[80][SPLIT2_COLS];
+    __shared__ uint64_t pad[MODE >= 4 ? 8960 : 1];   // MODE 4/5: 70 KB more LDS (one workgroup per CU)
+    if (MODE >= 4 && threadIdx.x == 0) pad[0] = n;
     const uint32_t wave = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const bool odd = lane & 1u;
     const uint32_t j = wave == 0 ? lane >> 1 : lane;
-    const uint32_t i = blockIdx.x * SPLIT2_MSGS + j;
+    // MODE 6: every workgroup of the grid hashes the same messages (redundant copies), records at
+    // rec + 16 * blockIdx.x
+    const uint32_t i = (MODE == 6 ? 0u : blockIdx.x * SPLIT2_MSGS) + j;
+    if (MODE == 6) rec += 16 * blockIdx.x;
     const bool live = j < SPLIT2_MSGS && i < n;
     const uint64_t L = live ? len[i] : 0;
     const uint8_t* m = base + (live ? off[i] : 0);
@@ -244,7 +250,7 @@ __global__ void __launch_bounds__(192) k_split2_x(uint32_t n, const uint8_t* bas
         }
     };
     const uint32_t k0 = par;
-    if (k0 < nb && MODE != 3) {
+    if (k0 < nb && MODE != 3 && MODE != 5) {
         if (MODE == 2) words(k0);
         else {
             sha512_load_block(m, L, k0, w);
@@ -257,7 +263,7 @@ __global__ void __launch_bounds__(192) k_split2_x(uint32_t n, const uint8_t* bas
     uint64_t busy = 0;
     for (uint32_t p = 0; p < nbmax; ++p) {
         const uint64_t ts = __builtin_amdgcn_s_memtime();
-        if (MODE != 3) {
+        if (MODE != 3 && MODE != 5) {
             if ((p & 1u) == par) {
                 const uint32_t k = p + 2;
                 if (k < nb) {
@@ -392,13 +398,15 @@ int main(int argc, char** argv) {
     {
         uint64_t* d_rec;
         CHECK(hipMalloc(&d_rec, 128));
-        for (int mode = 0; mode < 4; ++mode) {
+        for (int mode = 0; mode < 6; ++mode) {
             for (int rep = 0; rep < 8; ++rep) {
                 CHECK(hipEventRecord(e0, 0));
                 if (mode == 0) hipLaunchKernelGGL(k_split2_x<0>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
                 else if (mode == 1) hipLaunchKernelGGL(k_split2_x<1>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
                 else if (mode == 2) hipLaunchKernelGGL(k_split2_x<2>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
-                else hipLaunchKernelGGL(k_split2_x<3>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
+                else if (mode == 3) hipLaunchKernelGGL(k_split2_x<3>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
+                else if (mode == 4) hipLaunchKernelGGL(k_split2_x<4>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
+                else hipLaunchKernelGGL(k_split2_x<5>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
                 CHECK(hipEventRecord(e1, 0));
                 CHECK(hipEventSynchronize(e1));
                 float ms;
@@ -413,6 +421,28 @@ int main(int argc, char** argv) {
                        (uint32_t)(r[6] >> 4) & 3u, (uint32_t)(r[4] >> 13) & 7u, (uint32_t)(r[5] >> 13) & 7u,
                        (uint32_t)(r[6] >> 13) & 7u, (unsigned long long)r[8], (unsigned long long)r[9]);
             }
+        }
+    }
+    {   // redundant copies in one launch: does every workgroup run at the fast rate?
+        uint64_t* d_rec;
+        const int G = 16;
+        CHECK(hipMalloc(&d_rec, 128 * G));
+        for (int rep = 0; rep < 4; ++rep) {
+            CHECK(hipEventRecord(e0, 0));
+            hipLaunchKernelGGL(k_split2_x<6>, dim3(G), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
+            CHECK(hipEventRecord(e1, 0));
+            CHECK(hipEventSynchronize(e1));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            std::vector<uint64_t> r(16 * G);
+            CHECK(hipMemcpy(r.data(), d_rec, 128 * G, hipMemcpyDeviceToHost));
+            printf("{\"copies\": %d, \"rep\": %d, \"ms\": %.3f, \"round_cyc_per_block\": [", G, rep, ms);
+            for (int g = 0; g < G; ++g) printf("%s%.0f", g ? ", " : "", (double)r[16 * g] / nb);
+            printf("], \"cu\": [");
+            for (int g = 0; g < G; ++g) printf("%s%u", g ? ", " : "", (uint32_t)(r[16 * g + 4] >> 8) & 15u);
+            printf("], \"se\": [");
+            for (int g = 0; g < G; ++g) printf("%s%u", g ? ", " : "", (uint32_t)(r[16 * g + 4] >> 13) & 7u);
+            printf("]}\n");
         }
     }
     uint8_t dg[192];
