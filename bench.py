@@ -305,7 +305,8 @@ def digest_leg(eng, dev, n_node, n_share, reps, cpu_seconds, verify_step):
         assert bytes(got[b]) == hashlib.sha512(host[b].tobytes()).digest(), "GPU batch digest mismatch"
     padded = n_node * blocks * 128
     out["workload"] = "%d worker batches x %d B (977 x 512-B tx, bincode WorkerMessage::Batch)" % (n_node, blen)
-    out["kernel"] = "k_sha512_many (one lane per batch)"
+    out["kernel"] = ("k_sha512_split2 (one lane pair per batch, two schedule waves)" if n_node <= 32768
+                     else "k_sha512_many (one lane per batch)")
     out["GBps"] = n_node * blen / t / 1e9
     out["kernel_ms"] = t * 1e3
     out["roofline_hbm"] = {"achieved": padded / t / 1e9, "peak": 8000.0, "unit": "GB/s",
@@ -316,9 +317,8 @@ def digest_leg(eng, dev, n_node, n_share, reps, cpu_seconds, verify_step):
     t1 = lone[len(lone) // 2]
     out["single_chain"] = {"blocks_per_batch": blocks, "lone_batch_ms": t1 * 1e3, "ns_per_block": t1 / blocks * 1e9,
                            "best_ns_per_block": lone[0] / blocks * 1e9, "lone_batch_ms_all": [x * 1e3 for x in lone],
-                           "bound_GBps": {str(n): n * blen / t1 / 1e9 for n in (n_share, n_node)},
-                           "note": "a batch is one sequential chain of %d compressions: wall time >= lone-batch "
-                                   "time whatever the batch count, until the lanes exceed the SIMDs" % blocks}
+                           "note": "one batch alone on the GPU, median of 7 launches: a batch is one sequential chain "
+                                   "of %d compressions" % blocks}
     # C4 per-GPU share: 1,250 batches; alone, with the host->device copy from pinned memory, and
     # concurrently with the C2 verify step on a second stream
     pinned = torch.from_numpy(host[:n_share].reshape(-1)).pin_memory()
@@ -397,8 +397,11 @@ def worker_digest_leg(eng, n_batches=1250, windows=(32, 128, 1250), depth=2):
     out = {"batches": n_batches, "batch_bytes": blen, "depth": depth, "windows": {}}
     for win in windows:
         b = worker.DigestBatcher(eng, window=win, depth=depth)
-        for d, x in b.pipeline(rows[:min(2 * win, n_batches)]):   # warm the workspaces
+        # warm: depth + 2 windows, so every workspace the timed run can lease exists and is sized (a
+        # workspace's first use pays its pinned-buffer allocation and first DMAs, ~20 ms)
+        for d, x in b.pipeline(rows[:min((depth + 2) * win, n_batches)]):
             pass
+        rows = [r.copy() for r in rows]   # fresh host buffers, as a worker's received batches are
         t_push = {}
         lat = []
         t0 = time.perf_counter()

@@ -58,6 +58,8 @@ extern "C" {
 #define NW_F_R_SMALL 0x020u   /* R is of small order (meaningful when MATCH) */
 #define NW_F_SLOW 0x1000u     /* needed the exact batch equation (rare path) */
 #define NW_F_R_BAD 0x2000u    /* R failed to decode (found on the exact path) */
+/* Bits 0x4000 and above (other than the torsion coefficient at 0x700) are reserved: never set in
+ * returned flags.  A signature inside no certificate's vote range gets flags 0 (no verdict). */
 
 /* Opaque extended-point encoding exchanged between shards of one split batch
  * (nw_verify_batch_partial / nw_points_sum_is_identity): 160 bytes. */
@@ -153,7 +155,9 @@ int nw_points_sum_is_identity(nw_ctx* ctx, const uint8_t (*points)[NW_POINT_BYTE
 
 /* Certificate bulk path (Certificate::verify's batch step, primary/src/messages.rs:214, for many
  * certificates at once).  Signers are committee slots (nw_committee_load).  msg[c] is the 32-byte
- * certificate digest.  Outputs (each may be NULL):
+ * certificate digest.  Vote ranges must be pairwise disjoint (a vote's coefficient and exact-path
+ * term belong to one certificate): overlapping ranges are NW_ERR_ARG; a signature inside no range
+ * gets sig_ok 0 and affects no certificate.  Outputs (each may be NULL):
  *   cert_ok[c]        1 iff Signature::verify_batch(msg[c], votes of c) is Ok
  *   sig_ok[v]         1 iff verify_strict accepts vote v (the per-signature fallback bitmap)
  *   accepted_stake[c] sum of signer stake over votes with sig_ok = 1
@@ -176,8 +180,8 @@ int nw_verify_batches(nw_ctx* ctx, size_t nb, const uint32_t* first, const uint3
 /* Device-resident variant for streaming use (inputs already in HBM).  All pointers are device
  * pointers; ``stream`` is a hipStream_t (NULL = default stream).  ``sig_flags`` (uint32 per vote,
  * NW_F_* bits) may be NULL.  The inputs are checked on the device (every vote range inside
- * [0, nsigs), every signer slot inside the key cache); the kernels clamp them, so bad inputs never
- * fault — their signatures and certificates are rejected.
+ * [0, nsigs), no vote inside two ranges, every signer slot inside the key cache); the kernels clamp
+ * them, so bad inputs never fault — their signatures and certificates are rejected.
  *   d_status == NULL: the check is synchronous — the call waits for it on ``stream`` and returns
  *                     NW_ERR_ARG (enqueueing nothing else) when it fails; otherwise it enqueues the
  *                     verification and returns.

@@ -307,7 +307,8 @@ static constexpr int PREC_FLAGS_ROW = 20;
 static_assert(PREC_ROWS <= PBUF_WORDS, "pbuf workspace rows");
 static constexpr uint32_t PF_YMATCH = 1u << 20;   // internal: y_R Z == Y (projective)
 static constexpr uint32_t PF_RSIGN = 1u << 21;    // internal: R's sign bit (bit 255)
-static constexpr uint32_t PF_INTERNAL = PF_YMATCH | PF_RSIGN;
+static constexpr uint32_t PF_NOCERT = 1u << 22;   // internal: the signature is in no certificate's range
+static constexpr uint32_t PF_INTERNAL = PF_YMATCH | PF_RSIGN | PF_NOCERT;
 
 NW_HD void store_prec_soa(uint32_t* p, size_t n, size_t g, const ge_p3& P, uint32_t pflags) {
     store_fe_soa(p, n, g, P.X);

@@ -98,6 +98,11 @@ __global__ void __launch_bounds__(256, 4) k_sha512_many(uint32_t n, const uint8_
 
 // ------------------------------------------------------------------------------------ schedule / round split
 static constexpr uint32_t SPLIT_MAX_N = 32768;    // above: k_sha512_many (every SIMD has work anyway)
+// Unused dynamic LDS reserved by each k_sha512_split2 workgroup (variant builds only: with enough of
+// it no other kernel's workgroup fits on a digest workgroup's CU, tools/build_variants.sh).
+#ifndef NW_SHA_LDS_PAD
+#define NW_SHA_LDS_PAD 0
+#endif
 
 // ------------------------------------------------------------------------------------ two-lane split
 // The rounds on lane pairs (nw_sha512_2l.h: 20 instructions per round for one message instead of
@@ -176,8 +181,16 @@ __global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t
     const bool odd = lane & 1u;
     // rounds: lane pair (2j, 2j+1) -> message j; schedule: lane j < 32 -> message j
     const uint32_t j = wave == 0 ? lane >> 1 : lane;
-    const uint32_t i = blockIdx.x * SPLIT2_MSGS + j;
+    // A workgroup with fewer than 32 messages (a lone header or worker batch) fills its idle lane
+    // pairs with duplicate chains of its own messages, so the round wave always runs with a full
+    // EXEC mask: with 2 of 64 lanes active the same instruction stream took 9.1-16.7 k cycles per
+    // block depending on the CU, with every lane active 8.94-8.97 k on every CU
+    // (profiles/r04/sha_lone_r04j.jsonl, x_mode 0 vs 7).  Only the owning lanes write a digest.
+    const uint32_t wg_n = min(SPLIT2_MSGS, n - blockIdx.x * SPLIT2_MSGS);   // >= 1: grid = ceil(n / 32)
+    const uint32_t jm = j < SPLIT2_MSGS ? j % wg_n : j;
+    const uint32_t i = blockIdx.x * SPLIT2_MSGS + jm;
     const bool live = j < SPLIT2_MSGS && i < n;
+    const bool owner = live && jm == j;
     const uint64_t L = live ? len[i] : 0;
     const uint8_t* m = base + (live ? off[i] : 0);
     const uint32_t nb = live ? sha512_nblocks(L) : 0u;
@@ -224,7 +237,7 @@ __global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t
             }
             return;
         }
-        if (live) {
+        if (owner) {
             // odd lane: a b c d = digest bytes 0..31; even lane: e f g h = bytes 32..63
             uint4* o = reinterpret_cast<uint4*>(out + (size_t)i * 64 + (odd ? 0 : 32));
             uint32_t d[8];
@@ -273,8 +286,14 @@ hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* o
                               uint8_t* out, hipStream_t st) {
     if (n == 0) return hipSuccess;
     if (n <= SPLIT_MAX_N) {
-        hipLaunchKernelGGL(k_sha512_split2<0>, dim3(blocks_for(n, SPLIT2_MSGS)), dim3(192), 0, st, n, base, off, len,
-                           out);
+        if (NW_SHA_LDS_PAD > 0) {
+            static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sha512_split2<0>),
+                                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                               NW_SHA_LDS_PAD);
+            if (attr != hipSuccess) return attr;
+        }
+        hipLaunchKernelGGL(k_sha512_split2<0>, dim3(blocks_for(n, SPLIT2_MSGS)), dim3(192), NW_SHA_LDS_PAD, st, n, base,
+                           off, len, out);
     } else {
         hipLaunchKernelGGL(k_sha512_many, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, base, off, len, out);
     }

@@ -112,8 +112,13 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
 // g = L, L + NL, L + 2 NL, ... so every pbuf / pre access of a wave is one contiguous 256-B run.
 __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
     const uint32_t NL = (a.gn + a.fk - 1) / a.fk;
-    const uint32_t L = blockIdx.x * blockDim.x + threadIdx.x;
-    if (L >= NL) return;
+    const uint32_t Lr = blockIdx.x * blockDim.x + threadIdx.x;
+    // fewer lanes than a wave (one header or vote signature: ONE inversion on one lane): the idle
+    // lanes of wave 0 run duplicates (no writes), since a wave with a sparse EXEC mask issues its
+    // chain 1.2-1.4x slower
+    if (Lr >= NL && (NL >= 64 || Lr >= 64)) return;
+    const bool owner = Lr < NL;
+    const uint32_t L = owner ? Lr : Lr % NL;
     const uint32_t cnt = (a.gn - L + NL - 1) / NL;   // columns g0 + L + k NL < g0 + gn  (cnt <= fk)
     const size_t n = a.n;
     const size_t gbase = (size_t)a.g0 + L;
@@ -127,7 +132,7 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
         if ((uint32_t)k < cnt) {
             const size_t g = gbase + (size_t)k * NL;
             acc = fe_mul(acc, load_fe_soa(zrow, n, g));
-            store_fe_soa(a.pre, n, g, acc);
+            store_fe_soa(a.pre, n, g, acc);   // duplicates store the owner's own values (scratch)
         }
     }
     // Inversion: variable-time safegcd (public data) when each lane chains several signatures
@@ -150,15 +155,16 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
                 inv = fe_mul(inv, load_fe_soa(zrow, n, g));
             }
             const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
-            uint32_t f = finish_x_flags(load_fe_soa(a.pbuf, n, g), zi, a.pbuf[PREC_FLAGS_ROW * n + g]);
+            const uint32_t pf = a.pbuf[PREC_FLAGS_ROW * n + g];
+            uint32_t f = finish_x_flags(load_fe_soa(a.pbuf, n, g), zi, pf);
+            if (!owner) continue;
             if (a.batch_mode) {
-                const uint32_t cert = a.sig_cert[i];
-                if (cert == NO_CERT) {
+                if (pf & PF_NOCERT) {
                     f = 0u;   // inside no certificate's range: no message, no verdict, no exact-path entry
                 } else if ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) {
                     // the certificate is rejected (dalek: parse / decode error before the MSM): no
                     // exact-path work for any of its votes
-                    atomicOr(&a.cert_state[cert], CS_DOOM);
+                    atomicOr(&a.cert_state[a.sig_cert[i]], CS_DOOM);
                 } else if (!(f & NW_F_MATCH)) {
                     f |= NW_F_SLOW;
                     const uint32_t t = atomicAdd(a.slow_count, 1u);
@@ -374,8 +380,15 @@ __global__ void __launch_bounds__(256) k_slow_mul(VerifyParams a) {
     const uint32_t qd = threadIdx.x >> 2, q = threadIdx.x & 3u;
     uint32_t (*T)[40] = tab[qd];
     // entries dealt to the blocks first (one wave each), as in k_slow_prep: a wave's time is one
-    // chain whatever its number of quads, so spreading the entries keeps the waves short and apart
-    for (uint32_t t = qd * gridDim.x + blockIdx.x; t < cnt; t += gridDim.x * SLOW_MUL_QUADS) {
+    // chain whatever its number of quads, so spreading the entries keeps the waves short and apart.
+    // A wave with fewer entries than quads runs duplicate chains of its own entries on the idle
+    // quads (own LDS table slot, no record writes), so its EXEC mask stays full.
+    const uint32_t wq = (threadIdx.x & 63u) >> 2;                    // quad index inside the wave
+    for (uint32_t base = (qd - wq) * gridDim.x + blockIdx.x; base < cnt; base += gridDim.x * SLOW_MUL_QUADS) {
+        const uint32_t t_own = base + wq * gridDim.x;
+        const uint32_t v = (uint32_t)__popcll(__ballot(t_own < cnt)) >> 2;   // entries of this wave: quads [0, v)
+        const bool owner = wq < v;
+        const uint32_t t = owner ? t_own : base + (wq % v) * gridDim.x;
         uint32_t* rec = a.slow_buf + (size_t)t * SLOW_WORDS;
         if (rec[SLOW_KIND] != SK_BIG) continue;                      // uniform over the quad
         const uint32_t i = a.slow_list[t];
@@ -419,7 +432,7 @@ __global__ void __launch_bounds__(256) k_slow_mul(VerifyParams a) {
                 acc = ge_add_quad(acc, d < 0 ? ge_neg(e) : e);
             }
         }
-        if (q == 0) {
+        if (q == 0 && owner) {
             store_p3(rec, acc);
             rec[SLOW_KIND] = SK_MUL;
         }

@@ -145,8 +145,12 @@ NW_HD ge_p3 ge_scalarmult_w4(const uint32_t k_in[8], const ge_p3& Q, uint32_t* t
 // ge_scalarmult_w4; writes the same (X, Z, partial flags) record as k_verify, so k_finish completes
 // the strict verdict.  Semantics are those of k_verify with a cached key (nw_core.h).
 __global__ void __launch_bounds__(256) k_verify_var(VerifyParams a, uint32_t* scratch) {
-    const uint32_t gid = a.g0 + blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= a.g0 + a.gn) return;
+    // fewer signatures than a wave (one strict call): the idle lanes of wave 0 run duplicates, so the
+    // chain issues at the full-EXEC rate; they store only what their owner stores
+    const uint32_t graw = blockIdx.x * blockDim.x + threadIdx.x;
+    if (graw >= a.gn && (a.gn >= 64 || graw >= 64)) return;
+    const bool owner = graw < a.gn;
+    const uint32_t gid = a.g0 + (owner ? graw : graw % a.gn);
     const uint32_t i = gid;
     uint32_t R[8], S[8], Aw[8], h[8];
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
@@ -176,7 +180,7 @@ __global__ void __launch_bounds__(256) k_verify_var(VerifyParams a, uint32_t* sc
     P = ge_add(P, ge_cached_neg(ge_to_cached(hA)));
     asm volatile("" ::: "memory");
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
-    store_prec_soa(a.pbuf, a.n, gid, P, verify_pflags(P, R, frow[gid]));
+    if (owner) store_prec_soa(a.pbuf, a.n, gid, P, verify_pflags(P, R, frow[gid]));
 }
 
 // ------------------------------------------------------------------------------------ MSM

@@ -11,9 +11,10 @@
 
 namespace nw {
 
-// Signature i's inputs and h = SHA-512(R || A || M) mod l.
+// Signature i's inputs and h = SHA-512(R || A || M) mod l.  cert is clamped to a valid index; the
+// returned bool says the signature lies in no certificate's range (NO_CERT: it gets no verdict).
 template <int MSGMODE>
-__device__ __forceinline__ void lane_inputs(const VerifyParams& a, uint32_t i, uint32_t R[8], uint32_t S[8],
+__device__ __forceinline__ bool lane_inputs(const VerifyParams& a, uint32_t i, uint32_t R[8], uint32_t S[8],
                                             uint32_t& slot, uint32_t& kinfo, uint32_t& cert, uint32_t h[8]) {
     uint32_t Aw[8];
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
@@ -24,7 +25,8 @@ __device__ __forceinline__ void lane_inputs(const VerifyParams& a, uint32_t i, u
     load_w8(Aw, a.keys_raw + (size_t)slot * 8);
     kinfo = in_cache ? a.key_info[slot] : 0u;
     cert = a.sig_cert[i];
-    cert = cert == NO_CERT ? 0u : cert;   // a vote outside every range: k_finish gives it no verdict
+    const bool nocert = cert == NO_CERT;   // a vote outside every range: k_finish gives it no verdict
+    cert = nocert ? 0u : cert;
     if (MSGMODE == 0) {
         uint32_t M[8];
         load_w8(M, reinterpret_cast<const uint32_t*>(a.cert_msg) + (size_t)cert * 8);
@@ -34,6 +36,7 @@ __device__ __forceinline__ void lane_inputs(const VerifyParams& a, uint32_t i, u
         hram_generic(hw, R, Aw, a.msg_base + a.msg_off[i], a.msg_len[i]);
         sc_reduce512(h, hw);
     }
+    return nocert;
 }
 
 // A signature whose y does not match R's (so D_i = R_i - P_i != O: it will take the exact batch
@@ -66,10 +69,11 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     // signer-grouped order: the 64 lanes of a wave mostly share one key table (TLB / cache locality)
     const uint32_t i = a.perm ? a.perm[gid] : gid;
     uint32_t R[8], S[8], h[8], slot, kinfo, cert;
-    lane_inputs<MSGMODE>(a, i, R, S, slot, kinfo, cert, h);
+    const bool nocert = lane_inputs<MSGMODE>(a, i, R, S, slot, kinfo, cert, h);
     const bool sok = sc_is_canonical(S);
     const bool aok = (kinfo & KI_OK) != 0;
-    uint32_t flags = (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | ((kinfo & KI_SMALL) ? NW_F_A_SMALL : 0u);
+    uint32_t flags = (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | ((kinfo & KI_SMALL) ? NW_F_A_SMALL : 0u) |
+                     (nocert ? PF_NOCERT : 0u);
     const uint32_t tk = (kinfo >> KI_TORSION_SHIFT) & 7u;
     if (a.batch_mode && tk != 0 && sok && aok) {   // torsion keys only (never for honest committees)
         uint32_t z4[4];
@@ -138,16 +142,23 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
     // thousand entries of an adversarial batch land on wave 0 of every block, one working wave per
     // CU, instead of filling the first blocks' four waves, which the dispatcher may pack two or three
     // to a SIMD (each entry is a long serial chain: sharing a SIMD stretched the kernel 3x,
-    // measured at C5 with per-entry timestamps).
+    // measured at C5 with per-entry timestamps).  A wave with fewer entries than lanes runs
+    // duplicate chains of its own entries on the idle lanes (no writes): a wave with a sparse EXEC
+    // mask issues its chain up to 1.8x slower on some CUs.
     const uint32_t nthr = gridDim.x * blockDim.x;
-    for (uint32_t t = threadIdx.x * gridDim.x + blockIdx.x; t < cnt; t += nthr) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t base = (threadIdx.x - lane) * gridDim.x + blockIdx.x; base < cnt; base += nthr) {   // wave-uniform
+        const uint32_t t_own = base + lane * gridDim.x;
+        const uint32_t v = (uint32_t)__popcll(__ballot(t_own < cnt));   // entries of this wave: lanes [0, v)
+        const bool owner = lane < v;
+        const uint32_t t = owner ? t_own : base + (lane % v) * gridDim.x;
         const uint32_t i = a.slow_list[t];
         uint32_t* rec = a.slow_buf + (size_t)t * SLOW_WORDS;
         const uint32_t cert = a.sig_cert[i];   // slow-list entries always have an owner (k_finish)
         const uint32_t fi = a.flags[i];
-        a.flags[i] = fi & ~NW_F_P_SAVED;       // internal bit: never returned to the caller
+        if (owner) a.flags[i] = fi & ~NW_F_P_SAVED;   // internal bit: never returned to the caller
         if (a.cert_state[cert] & CS_DOOM) {
-            rec[SLOW_KIND] = SK_SKIP;
+            if (owner) rec[SLOW_KIND] = SK_SKIP;
             continue;
         }
         uint32_t R[8];
@@ -157,9 +168,11 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
 #endif
         ge_p3 Rp;
         if (!ge_decompress(Rp, R)) {
-            a.flags[i] = (fi & ~NW_F_P_SAVED) | NW_F_R_BAD;
-            atomicOr(&a.cert_state[cert], CS_DOOM);
-            rec[SLOW_KIND] = SK_SKIP;
+            if (owner) {
+                a.flags[i] = (fi & ~NW_F_P_SAVED) | NW_F_R_BAD;
+                atomicOr(&a.cert_state[cert], CS_DOOM);
+                rec[SLOW_KIND] = SK_SKIP;
+            }
             continue;
         }
 #ifdef NW_SLOW_TIMING
@@ -184,24 +197,27 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
         const bool small = ge_is_identity(ge_dbl(D4));
 #ifdef NW_SLOW_TIMING
         const uint64_t tm3 = __builtin_amdgcn_s_memtime();
-        printf("slow_prep t=%u saved=%d dec=%llu P=%llu Dz8=%llu small=%d rt0=%llu rt1=%llu\n", t,
-               (fi & NW_F_P_SAVED) ? 1 : 0, (unsigned long long)(tm1 - tm0), (unsigned long long)(tm2 - tm1),
-               (unsigned long long)(tm3 - tm2), small ? 1 : 0, (unsigned long long)rt_start,
-               (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        if (owner)
+            printf("slow_prep t=%u saved=%d dec=%llu P=%llu Dz8=%llu small=%d rt0=%llu rt1=%llu\n", t,
+                   (fi & NW_F_P_SAVED) ? 1 : 0, (unsigned long long)(tm1 - tm0), (unsigned long long)(tm2 - tm1),
+                   (unsigned long long)(tm3 - tm2), small ? 1 : 0, (unsigned long long)rt_start,
+                   (unsigned long long)__builtin_amdgcn_s_memrealtime());
 #endif
         const uint32_t kind = (small || zzero) ? SK_SMALL : SK_BIG;
         if (kind == SK_BIG) {
-            atomicAdd(&a.cert_state[cert], 1u);
-            store_p3(rec, D);
+            if (owner) {
+                atomicAdd(&a.cert_state[cert], 1u);
+                store_p3(rec, D);
+            }
         } else {
             // the term itself: z_i D_i = (z_i mod 8) D_i from D, 2D, 4D (k_cert_exact only adds records)
             const uint32_t z8 = zzero ? 0u : (z4[0] & 7u);
-            ge_p3 t = ge_select(ge_identity(), D, (z8 & 1u) != 0);
-            t = ge_add(t, ge_to_cached(ge_select(ge_identity(), D2, (z8 & 2u) != 0)));
-            t = ge_add(t, ge_to_cached(ge_select(ge_identity(), D4, (z8 & 4u) != 0)));
-            store_p3(rec, t);
+            ge_p3 t8 = ge_select(ge_identity(), D, (z8 & 1u) != 0);
+            t8 = ge_add(t8, ge_to_cached(ge_select(ge_identity(), D2, (z8 & 2u) != 0)));
+            t8 = ge_add(t8, ge_to_cached(ge_select(ge_identity(), D4, (z8 & 4u) != 0)));
+            if (owner) store_p3(rec, t8);
         }
-        rec[SLOW_KIND] = kind;
+        if (owner) rec[SLOW_KIND] = kind;
     }
 }
 

@@ -18,6 +18,7 @@ import torch  # noqa: E402,F401  (before libnwcrypto: shared HIP runtime)
 
 def main():
     passes = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+    no_gc = "nogc" in sys.argv[2:]   # Python's cyclic GC off during the timed passes
     from narwhal_amd import _lib, workload
     torch.cuda.set_device(0)
     eng = _lib.Engine(device=0, key_window=-1)
@@ -53,7 +54,11 @@ def main():
                         "start_ms": (t0 - t_origin) * 1e3, "ms": (t1 - t0) * 1e3})
         return bool(ok.all())
 
-    out = {"passes": []}
+    out = {"passes": [], "gc_disabled": no_gc}
+    import gc
+    gc.collect()
+    if no_gc:
+        gc.disable()
     with ThreadPoolExecutor(threads) as ex:
         assert all(ex.map(lambda kp: run(kp[0], kp[1], -1), enumerate(parts)))
         for rep in range(passes):

@@ -176,7 +176,11 @@ __global__ void __launch_bounds__(192) k_split2_x(uint32_t n, const uint8_t* bas
     const uint32_t j = wave == 0 ? lane >> 1 : lane;
     // MODE 6: every workgroup of the grid hashes the same messages (redundant copies), records at
     // rec + 16 * blockIdx.x
-    const uint32_t i = (MODE == 6 ? 0u : blockIdx.x * SPLIT2_MSGS) + j;
+    // MODE 7: a workgroup with fewer than 32 messages fills its idle lane pairs with duplicate chains
+    // of its own messages (every lane active: the EXEC-mask test)
+    const uint32_t wg_n = n - blockIdx.x * SPLIT2_MSGS < SPLIT2_MSGS ? n - blockIdx.x * SPLIT2_MSGS : SPLIT2_MSGS;
+    const uint32_t jj = (MODE == 7 && j < SPLIT2_MSGS) ? j % wg_n : j;
+    const uint32_t i = (MODE == 6 ? 0u : blockIdx.x * SPLIT2_MSGS) + jj;
     if (MODE == 6) rec += 16 * blockIdx.x;
     const bool live = j < SPLIT2_MSGS && i < n;
     const uint64_t L = live ? len[i] : 0;
@@ -398,7 +402,8 @@ int main(int argc, char** argv) {
     {
         uint64_t* d_rec;
         CHECK(hipMalloc(&d_rec, 128));
-        for (int mode = 0; mode < 6; ++mode) {
+        for (int mode = 0; mode < 8; ++mode) {
+            if (mode == 6) continue;
             for (int rep = 0; rep < 8; ++rep) {
                 CHECK(hipEventRecord(e0, 0));
                 if (mode == 0) hipLaunchKernelGGL(k_split2_x<0>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
@@ -406,7 +411,8 @@ int main(int argc, char** argv) {
                 else if (mode == 2) hipLaunchKernelGGL(k_split2_x<2>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
                 else if (mode == 3) hipLaunchKernelGGL(k_split2_x<3>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
                 else if (mode == 4) hipLaunchKernelGGL(k_split2_x<4>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
-                else hipLaunchKernelGGL(k_split2_x<5>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
+                else if (mode == 5) hipLaunchKernelGGL(k_split2_x<5>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
+                else hipLaunchKernelGGL(k_split2_x<7>, dim3(1), dim3(192), 0, 0, 1u, d_msg, d_off, d_len, d_rec);
                 CHECK(hipEventRecord(e1, 0));
                 CHECK(hipEventSynchronize(e1));
                 float ms;

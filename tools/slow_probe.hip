@@ -1,5 +1,7 @@
 // Lone-wave cost of the serial chains on the exact batch path and the latency path: how many
-// shader cycles one wave (all 64 lanes busy on independent data) spends on each building block.
+// shader cycles one wave spends on each building block, with all 64 lanes busy on independent data
+// and with only the first 4 or 1 lanes active (the EXEC mask of k_slow_mul's quad / k_slow_prep's
+// lane / k_finish's single inversion), over 8 launches each (different CUs).
 // One workgroup of 64 threads per variant; s_memtime around the timed region.
 //   fe_sq x254         the square-root / inversion exponent chain (fe_pow22523 is 250 + 11)
 //   fe_mul x100        generic product
@@ -44,9 +46,10 @@ __device__ void sink(uint32_t* out, const fe& f) {
 }
 
 template <int V>
-__global__ void __launch_bounds__(64) k_probe(uint32_t* out, uint64_t* cyc, uint32_t salt) {
+__global__ void __launch_bounds__(64) k_probe(uint32_t* out, uint64_t* cyc, uint32_t salt, uint32_t act) {
     fe f = fe_seed(threadIdx.x + salt);
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x < act) {
     if (V == 0) {
         f = fe_sqn(f, 254);
         sink(out, f);
@@ -77,29 +80,39 @@ __global__ void __launch_bounds__(64) k_probe(uint32_t* out, uint64_t* cyc, uint
     } else {
         sink(out, fe_invert_sg(f));
     }
+    }
     const uint64_t t1 = __builtin_amdgcn_s_memtime();
-    if (threadIdx.x == 0) cyc[V] = t1 - t0;
+    if (threadIdx.x == 0) {
+        cyc[2 * V] = t1 - t0;
+        cyc[2 * V + 1] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    }
 }
 
 int main() {
     uint32_t* d_out;
     uint64_t* d_cyc;
     CHECK(hipMalloc(&d_out, 4096));
-    CHECK(hipMalloc(&d_cyc, 64));
     const char* names[7] = {"fe_sq_x254", "fe_mul_x100", "ge_decompress", "ge_dbl_x128", "ge_dbl_quad_x128",
                             "fe_invert_var", "fe_invert_sg"};
-    for (int rep = 0; rep < 2; ++rep) {
-        hipLaunchKernelGGL(k_probe<0>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep);
-        hipLaunchKernelGGL(k_probe<1>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep);
-        hipLaunchKernelGGL(k_probe<2>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep);
-        hipLaunchKernelGGL(k_probe<3>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep);
-        hipLaunchKernelGGL(k_probe<4>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep);
-        hipLaunchKernelGGL(k_probe<5>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep);
-        hipLaunchKernelGGL(k_probe<6>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep);
-        CHECK(hipDeviceSynchronize());
+    CHECK(hipMalloc(&d_cyc, 256));
+    const uint32_t acts[3] = {64, 4, 1};
+    for (int a = 0; a < 3; ++a) {
+        for (int rep = 0; rep < 8; ++rep) {
+            const uint32_t act = acts[a];
+            hipLaunchKernelGGL(k_probe<0>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep, act);
+            hipLaunchKernelGGL(k_probe<1>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep, act);
+            hipLaunchKernelGGL(k_probe<2>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep, act);
+            hipLaunchKernelGGL(k_probe<3>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep, act);
+            hipLaunchKernelGGL(k_probe<4>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep, act);
+            hipLaunchKernelGGL(k_probe<5>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep, act);
+            hipLaunchKernelGGL(k_probe<6>, dim3(1), dim3(64), 0, 0, d_out, d_cyc, rep, act);
+            CHECK(hipDeviceSynchronize());
+            uint64_t cyc[16];
+            CHECK(hipMemcpy(cyc, d_cyc, 128, hipMemcpyDeviceToHost));
+            for (int v = 0; v < 7; ++v)
+                printf("{\"probe\": \"%s\", \"active_lanes\": %u, \"rep\": %d, \"cycles\": %llu, \"cu\": %u}\n",
+                       names[v], act, rep, (unsigned long long)cyc[2 * v], (uint32_t)(cyc[2 * v + 1] >> 8) & 15u);
+        }
     }
-    uint64_t cyc[8];
-    CHECK(hipMemcpy(cyc, d_cyc, 64, hipMemcpyDeviceToHost));
-    for (int v = 0; v < 7; ++v) printf("{\"probe\": \"%s\", \"cycles\": %llu}\n", names[v], (unsigned long long)cyc[v]);
     return 0;
 }
