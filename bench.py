@@ -399,7 +399,7 @@ def worker_digest_leg(eng, n_batches=1250, windows=(32, 128, 1250), depth=2):
         b = worker.DigestBatcher(eng, window=win, depth=depth)
         # warm: depth + 2 windows, so every workspace the timed run can lease exists and is sized (a
         # workspace's first use pays its pinned-buffer allocation and first DMAs, ~20 ms)
-        for d, x in b.pipeline(rows[:min((depth + 2) * win, n_batches)]):
+        for d, x in b.pipeline([rows[k % n_batches] for k in range((depth + 2) * win)]):
             pass
         rows = [r.copy() for r in rows]   # fresh host buffers, as a worker's received batches are
         t_push = {}
@@ -511,6 +511,9 @@ def parse_args(argv):
     ap.add_argument("--digest-batches", type=int, default=10000, help="0 disables the digest leg")
     ap.add_argument("--digest-share", type=int, default=1250, help="C4 per-GPU batch share")
     ap.add_argument("--no-extras", action="store_true", help="headline only (no host_fed / msm / latency legs)")
+    ap.add_argument("--streams", type=int, default=2,
+                    help="batches in flight: step i runs on stream i mod S with its own output buffers, so one "
+                         "batch's k_finish / slow path overlaps the next batch's k_verify (1: strictly serial)")
     ap.add_argument("--key-window", type=int, default=-1,
                     help="key comb window; -1 = committee mode (library sizes it for the loaded committee)")
     ap.add_argument("--dry-run", action="store_true",
@@ -695,16 +698,20 @@ def main(argv=None):
     d_first = torch.from_numpy(cs.cert_first.astype(np.int32)).to(dev)
     d_n = torch.from_numpy(cs.cert_n.astype(np.int32)).to(dev)
     d_msg = torch.from_numpy(cs.msgs).to(dev)
-    d_ok = torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev)
-    d_flags = torch.zeros(cs.nsigs, dtype=torch.int32, device=dev)
-    d_stake = torch.zeros(cs.ncerts, dtype=torch.int64, device=dev)
-    d_status = torch.zeros(1, dtype=torch.int32, device=dev)   # asynchronous input check (NW_OK / NW_ERR_ARG)
+    # one output set per batch in flight (verdicts, flags, accepted stake, input-check status)
+    nst = max(1, args.streams)
+    outs = [dict(ok=torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev),
+                 flags=torch.zeros(cs.nsigs, dtype=torch.int32, device=dev),
+                 stake=torch.zeros(cs.ncerts, dtype=torch.int64, device=dev),
+                 status=torch.zeros(1, dtype=torch.int32, device=dev)) for _ in range(nst)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(nst - 1)]
     zseed = os.urandom(32)
 
-    def verify_step(stream):
+    def verify_step(stream, o=outs[0]):
         eng.verify_certs_dev(cs.ncerts, d_first.data_ptr(), d_n.data_ptr(), cs.nsigs, d_sig.data_ptr(),
-                             d_signer.data_ptr(), d_msg.data_ptr(), zseed, first_cert, d_ok.data_ptr(),
-                             d_flags.data_ptr(), d_stake.data_ptr(), stream.cuda_stream, d_status=d_status.data_ptr())
+                             d_signer.data_ptr(), d_msg.data_ptr(), zseed, first_cert, o["ok"].data_ptr(),
+                             o["flags"].data_ptr(), o["stake"].data_ptr(), stream.cuda_stream,
+                             d_status=o["status"].data_ptr())
 
     # C4: the rank's worker-batch digests (worker/src/processor.rs:65) run inside the timed step on
     # a second stream, concurrently with the verify kernels; the step ends when both are done
@@ -716,31 +723,47 @@ def main(argv=None):
         d_bdata = torch.from_numpy(host_b.reshape(-1)).to(dev)
         d_boff = torch.arange(ndig, dtype=torch.int64, device=dev) * blen
         d_blen = torch.full((ndig,), blen, dtype=torch.int64, device=dev)
-        d_bout = torch.empty((ndig, 64), dtype=torch.uint8, device=dev)
-        s_dig = torch.cuda.Stream(device=dev)
-        ev_dig = torch.cuda.Event()
+        d_bouts = [torch.empty((ndig, 64), dtype=torch.uint8, device=dev) for _ in range(nst)]
+        # one digest stream per batch in flight: step i's digests overlap step i + 1's
+        s_digs = [torch.cuda.Stream(device=dev) for _ in range(nst)]
+        ev_digs = [torch.cuda.Event() for _ in range(nst)]
+
+    # N > 1: every all_gather on one stream (collectives of one communicator stay serialized), after
+    # its batch's kernels; a stream reuses its output set only after that set's all_gather
+    s_comm = torch.cuda.Stream(device=dev) if world > 1 and nst > 1 else None
+    n_step = [0]
 
     def step():
-        cur = torch.cuda.current_stream()
+        i = n_step[0]
+        n_step[0] += 1
+        cur, o = streams[i % nst], outs[i % nst]
         if ndig:
+            s_dig, ev_dig = s_digs[i % nst], ev_digs[i % nst]
             s_dig.wait_stream(cur)
-            eng.sha512_many_dev(d_bdata.data_ptr(), d_boff.data_ptr(), d_blen.data_ptr(), ndig, d_bout.data_ptr(),
-                                s_dig.cuda_stream)
+            eng.sha512_many_dev(d_bdata.data_ptr(), d_boff.data_ptr(), d_blen.data_ptr(), ndig,
+                                d_bouts[i % nst].data_ptr(), s_dig.cuda_stream)
             ev_dig.record(s_dig)
-        verify_step(cur)
+        verify_step(cur, o)
         if ndig:
             cur.wait_event(ev_dig)
         if world > 1:
-            shard.allgather_verdicts(d_ok, d_stake, ranges)   # RCCL all_gather of bitmaps + stake
+            if s_comm is None:
+                shard.allgather_verdicts(o["ok"], o["stake"], ranges)   # RCCL all_gather of bitmaps + stake
+            else:
+                s_comm.wait_stream(cur)
+                with torch.cuda.stream(s_comm):
+                    shard.allgather_verdicts(o["ok"], o["stake"], ranges)
+                cur.wait_stream(s_comm)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    ok_all = (bool(d_ok.all().item()) and bool((d_stake == plan["votes"]).all().item())
-              and int(d_status.item()) == 0)
+    ok_all = all(bool(o["ok"].all().item()) and bool((o["stake"] == plan["votes"]).all().item())
+                 and int(o["status"].item()) == 0 for o in outs[:min(nst, max(1, args.warmup))])
     if ndig:
         for b in (0, ndig - 1):
-            ok_all = ok_all and bytes(d_bout[b].cpu().numpy()) == hashlib.sha512(host_b[b].tobytes()).digest()
+            for d_bout in d_bouts[:min(nst, max(1, args.warmup))]:
+                ok_all = ok_all and bytes(d_bout[b].cpu().numpy()) == hashlib.sha512(host_b[b].tobytes()).digest()
     if world > 1:
         dist.barrier()
     eng.profile_read()             # discard warmup events

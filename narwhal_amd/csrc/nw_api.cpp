@@ -219,14 +219,28 @@ int fail(nw_ctx* c, hipError_t e, const char* what) {
 // user; ``finish(st)`` records the completion event (kept pending for asynchronous calls).  A
 // host-buffer call that fails after enqueueing synchronizes its stream on release, so no DMA from
 // its pinned buffer and no kernel on its scratch outlives the call.
+//
+// Which free workspace a call gets: one whose last work was on the call's own stream (stream order
+// already serializes them), else one with no work in flight, else a new one while the pool is below
+// kMaxWorkspaces.  So device-buffer calls alternating over two streams (one batch's k_finish and
+// slow path under the next batch's k_verify) run on two workspaces and never wait for each other;
+// only a full pool falls back to the most recently freed workspace and its completion event.
 class Lease {
 public:
-    explicit Lease(nw_ctx* ctx) : ctx_(ctx) {
+    explicit Lease(nw_ctx* ctx, hipStream_t st = nullptr) : ctx_(ctx) {
         std::unique_lock<std::mutex> g(ctx->pool_mu);
         for (;;) {
-            if (!ctx->free_ws.empty()) {
-                ws_ = ctx->free_ws.back();
-                ctx->free_ws.pop_back();
+            auto& fr = ctx->free_ws;
+            if (!fr.empty()) {
+                size_t pick = fr.size();
+                for (size_t i = fr.size(); i-- > 0 && pick == fr.size();)
+                    if (fr[i]->pending && st && fr[i]->last == st) pick = i;
+                for (size_t i = fr.size(); i-- > 0 && pick == fr.size();)
+                    if (!fr[i]->pending || hipEventQuery(fr[i]->done) == hipSuccess) pick = i;
+                if (pick == fr.size() && ctx->pool.size() < kMaxWorkspaces) break;   // all busy: a new one
+                if (pick == fr.size()) pick = fr.size() - 1;
+                ws_ = fr[pick];
+                fr.erase(fr.begin() + (ptrdiff_t)pick);
                 return;
             }
             if (ctx->pool.size() < kMaxWorkspaces) break;
@@ -1490,7 +1504,7 @@ int nw_verify_certs_dev(nw_ctx* ctx, size_t ncerts, const uint32_t* d_cert_first
         set_error(ctx, "nw_verify_certs_dev: no committee loaded (signer slots outside the empty key cache)");
         return NW_ERR_ARG;
     }
-    Lease lease(ctx);
+    Lease lease(ctx, st);
     Workspace* ws = lease.ws();
     if (!ws) return NW_ERR_DEVICE;
     NW_TRY(lease.bind(st, false), "hipStreamWaitEvent");

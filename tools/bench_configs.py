@@ -29,13 +29,16 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import numpy as np  # noqa: E402
 
 L = 2**252 + 27742317777372353535851937790883648493
+STREAMS = 2   # batches in flight (bench.py --streams); --streams overrides
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def time_gpu(eng, cs, slots, zseed, steps, warmup, cert_base=0):
+def time_gpu(eng, cs, slots, zseed, steps, warmup, cert_base=0, streams=2):
+    """ms per step with ``streams`` batches in flight (step i on stream i mod S, its own outputs);
+    the verdicts and flags returned are checked identical across the output sets."""
     import torch
     dev = torch.device("cuda", torch.cuda.current_device())
     d_sig = torch.from_numpy(cs.sigs).to(dev)
@@ -43,18 +46,21 @@ def time_gpu(eng, cs, slots, zseed, steps, warmup, cert_base=0):
     d_first = torch.from_numpy(cs.cert_first.astype(np.int32)).to(dev)
     d_n = torch.from_numpy(cs.cert_n.astype(np.int32)).to(dev)
     d_msg = torch.from_numpy(cs.msgs).to(dev)
-    d_ok = torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev)
-    d_flags = torch.zeros(cs.nsigs, dtype=torch.int32, device=dev)
-    d_stake = torch.zeros(cs.ncerts, dtype=torch.int64, device=dev)
-    d_status = torch.zeros(1, dtype=torch.int32, device=dev)
+    outs = [(torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev), torch.zeros(cs.nsigs, dtype=torch.int32, device=dev),
+             torch.zeros(cs.ncerts, dtype=torch.int64, device=dev), torch.zeros(1, dtype=torch.int32, device=dev))
+            for _ in range(streams)]
+    sts = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(streams - 1)]
+    n = [0]
 
     def step():
+        d_ok, d_flags, d_stake, d_status = outs[n[0] % streams]
+        st = sts[n[0] % streams]
+        n[0] += 1
         eng.verify_certs_dev(cs.ncerts, d_first.data_ptr(), d_n.data_ptr(), cs.nsigs, d_sig.data_ptr(),
                              d_signer.data_ptr(), d_msg.data_ptr(), zseed, cert_base, d_ok.data_ptr(),
-                             d_flags.data_ptr(), d_stake.data_ptr(), torch.cuda.current_stream().cuda_stream,
-                             d_status=d_status.data_ptr())
+                             d_flags.data_ptr(), d_stake.data_ptr(), st.cuda_stream, d_status=d_status.data_ptr())
 
-    for _ in range(warmup):
+    for _ in range(max(warmup, streams)):
         step()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -62,8 +68,10 @@ def time_gpu(eng, cs, slots, zseed, steps, warmup, cert_base=0):
         step()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
-    ok = d_ok.cpu().numpy().astype(bool)
-    flags = d_flags.cpu().numpy()
+    ok = outs[0][0].cpu().numpy().astype(bool)
+    flags = outs[0][1].cpu().numpy()
+    for o in outs[1:]:
+        assert (o[0].cpu().numpy().astype(bool) == ok).all() and (o[1].cpu().numpy() == flags).all()
     return dt, ok, flags
 
 
@@ -176,11 +184,13 @@ def run_cert_config(name, eng_factory, validators, ncerts, votes, steps, warmup,
     if adversarial:
         kinds = make_adversarial(cs, com, adversarial, np.random.default_rng(5))
     zseed = bytes(range(32))
-    dt, ok, flags = time_gpu(eng, cs, slots, zseed, steps, warmup)
+    dt1, _, _ = time_gpu(eng, cs, slots, zseed, steps, warmup, streams=1)
+    dt, ok, flags = time_gpu(eng, cs, slots, zseed, steps, warmup, streams=STREAMS)
     sel = list(range(0, ncerts, max(1, ncerts // parity_sample)))[:parity_sample]
     out = {"config": name, "validators": validators, "certs": ncerts, "votes_per_cert": votes,
            "sigs_per_step": int(cs.nsigs), "key_window": eng.key_window(), "committee_load_s": t_keys,
-           "ms_per_step": dt * 1e3, "sigs_per_s": cs.nsigs / dt,
+           "ms_per_step": dt * 1e3, "sigs_per_s": cs.nsigs / dt, "batches_in_flight": STREAMS,
+           "ms_per_step_serial": dt1 * 1e3, "sigs_per_s_serial": cs.nsigs / dt1,
            "certs_accepted": int(ok.sum()), "p50_cert_latency_ms": latency(eng, cs, slots, zseed)}
     out["parity"] = parity_certs(cs, com, ok, zseed, sel, threads)
     if kinds:
@@ -251,7 +261,9 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=5.0)
     ap.add_argument("--threads", type=int, default=int(os.environ.get("NW_CPU_THREADS", "16")))
+    ap.add_argument("--streams", type=int, default=STREAMS)
     args = ap.parse_args()
+    globals()["STREAMS"] = max(1, args.streams)
     import torch
     torch.cuda.set_device(0)
     from narwhal_amd import _lib
