@@ -484,12 +484,12 @@ def launch_ranks(args, argv):
 # the node's round, partitioned over the ranks by shard.partition (strong scaling: C3 =
 # configs[2], 1,000 certificates x 667 votes; config/src/lib.rs:189-194 gives the 2f+1 = 667).
 CONFIGS = {
-    "C2": {"validators": 100, "certs": 14926, "votes": 67, "scope": "rank", "digest_batches": 0,
+    "C2": {"validators": 100, "certs": 14926, "votes": 67, "scope": "rank", "digest_batches": 0, "streams": 2,
            "baseline": "configs[1]: 100-validator committee, 67-vote certificates, 1M signatures per MI355X"},
-    "C3": {"validators": 1000, "certs": 1000, "votes": 667, "scope": "node", "digest_batches": 0,
+    "C3": {"validators": 1000, "certs": 1000, "votes": 667, "scope": "node", "digest_batches": 0, "streams": 2,
            "baseline": "configs[2]: 1,000-validator committee, 667-vote certificates, sharded over the GPUs "
                        "with an RCCL verdict all-gather"},
-    "C4": {"validators": 10000, "certs": 1250, "votes": 6667, "scope": "rank", "digest_batches": 1250,
+    "C4": {"validators": 10000, "certs": 1250, "votes": 6667, "scope": "rank", "digest_batches": 1250, "streams": 1,
            "baseline": "configs[3]: 10,000-validator committee, 6,667-vote certificates plus worker 500 KB batch "
                        "SHA-512 digests; per GPU 1/8 of a node round (1,250 certificates, 1,250 batches)"},
 }
@@ -511,9 +511,11 @@ def parse_args(argv):
     ap.add_argument("--digest-batches", type=int, default=10000, help="0 disables the digest leg")
     ap.add_argument("--digest-share", type=int, default=1250, help="C4 per-GPU batch share")
     ap.add_argument("--no-extras", action="store_true", help="headline only (no host_fed / msm / latency legs)")
-    ap.add_argument("--streams", type=int, default=2,
+    ap.add_argument("--streams", type=int, default=None,
                     help="batches in flight: step i runs on stream i mod S with its own output buffers, so one "
-                         "batch's k_finish / slow path overlaps the next batch's k_verify (1: strictly serial)")
+                         "batch's k_finish / slow path overlaps the next batch's k_verify (1: strictly serial). "
+                         "Default per config: 2 for C2 / C3; 1 for C4, where two 8.3M-signature k_verify launches "
+                         "over 10,000 key tables slow each other down (r04o: 401 vs 466 M sigs/s)")
     ap.add_argument("--key-window", type=int, default=-1,
                     help="key comb window; -1 = committee mode (library sizes it for the loaded committee)")
     ap.add_argument("--dry-run", action="store_true",
@@ -699,7 +701,7 @@ def main(argv=None):
     d_n = torch.from_numpy(cs.cert_n.astype(np.int32)).to(dev)
     d_msg = torch.from_numpy(cs.msgs).to(dev)
     # one output set per batch in flight (verdicts, flags, accepted stake, input-check status)
-    nst = max(1, args.streams)
+    nst = max(1, args.streams if args.streams is not None else CONFIGS[args.config]["streams"])
     outs = [dict(ok=torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev),
                  flags=torch.zeros(cs.nsigs, dtype=torch.int32, device=dev),
                  stake=torch.zeros(cs.ncerts, dtype=torch.int64, device=dev),
@@ -792,6 +794,18 @@ def main(argv=None):
     total_sigs = plan["total_sigs"] * args.steps       # every rank's signatures (node-wide)
     value = total_sigs / elapsed
 
+    iso = None
+    if rank == 0 and nst > 1:
+        # k_verify alone (one batch at a time, after the timed region): with batches in flight the
+        # timed launches share the SIMDs with the other batch's kernels, so their durations are longer
+        # than the kernel's own
+        eng.profile_enable(True)
+        for _ in range(3):
+            verify_step(streams[0], outs[0])
+            torch.cuda.synchronize()
+        eng.profile_enable(False)
+        iso = eng.profile_read()
+
     if rank == 0:
         avg_launch_s = (kms / kn) / 1e3 if kn else float("nan")
         if ksigs is None:                              # library without nw_profile_read_sigs (A/B runs)
@@ -809,6 +823,12 @@ def main(argv=None):
             "traffic": traffic_per_launch() if args.config == "C2" else None,
             "per_cycle": clock_frac_profile() if args.config == "C2" else None,
             "avg_launch_ms": avg_launch_s * 1e3, "launches": kn,
+            "batches_in_flight": nst,
+            "isolated": None if not iso or not iso[1] else {
+                "avg_launch_ms": iso[0] / iso[1], "launches": iso[1],
+                "frac": sigs_per_launch * fm * MADS_PER_FM / (iso[0] / iso[1] / 1e3) / 1e12 / peak,
+                "note": "k_verify launched alone after the timed region (frac above: the timed launches, which "
+                        "overlap the other batch's k_finish / preamble)"},
             "work_model": "%.0f sigs/launch (%d launches per step) x %d FM/sig (7 FM per mixed addition x (%d basepoint "
                           "+ %d key - 1) comb positions + 1 FM for the chain's first entry, key window %d) x 100 u32 "
                           "MADs; SHA-512/mod-l/recoding VALU work not counted; peak = measured v_mad_u64_u32 rate"

@@ -172,7 +172,7 @@ def make_adversarial(cs, com, frac, rng):
 
 # ------------------------------------------------------------------------------ configs
 def run_cert_config(name, eng_factory, validators, ncerts, votes, steps, warmup, cpu_seconds, threads,
-                    adversarial=0.0, parity_sample=64):
+                    adversarial=0.0, parity_sample=64, streams=None):
     from narwhal_amd import workload
     eng = eng_factory()
     t0 = time.perf_counter()
@@ -185,11 +185,12 @@ def run_cert_config(name, eng_factory, validators, ncerts, votes, steps, warmup,
         kinds = make_adversarial(cs, com, adversarial, np.random.default_rng(5))
     zseed = bytes(range(32))
     dt1, _, _ = time_gpu(eng, cs, slots, zseed, steps, warmup, streams=1)
-    dt, ok, flags = time_gpu(eng, cs, slots, zseed, steps, warmup, streams=STREAMS)
+    streams = STREAMS if streams is None else streams
+    dt, ok, flags = time_gpu(eng, cs, slots, zseed, steps, warmup, streams=streams)
     sel = list(range(0, ncerts, max(1, ncerts // parity_sample)))[:parity_sample]
     out = {"config": name, "validators": validators, "certs": ncerts, "votes_per_cert": votes,
            "sigs_per_step": int(cs.nsigs), "key_window": eng.key_window(), "committee_load_s": t_keys,
-           "ms_per_step": dt * 1e3, "sigs_per_s": cs.nsigs / dt, "batches_in_flight": STREAMS,
+           "ms_per_step": dt * 1e3, "sigs_per_s": cs.nsigs / dt, "batches_in_flight": streams,
            "ms_per_step_serial": dt1 * 1e3, "sigs_per_s_serial": cs.nsigs / dt1,
            "certs_accepted": int(ok.sum()), "p50_cert_latency_ms": latency(eng, cs, slots, zseed)}
     out["parity"] = parity_certs(cs, com, ok, zseed, sel, threads)
@@ -283,7 +284,7 @@ def main():
                                 adversarial=0.01, parity_sample=1000)
         elif name == "C4":
             r = run_cert_config("C4", fac, 10000, 1250, 6667, max(2, args.steps // 2), 1, args.cpu_seconds,
-                                args.threads, parity_sample=16)
+                                args.threads, parity_sample=16, streams=1)   # see bench.py --streams
         elif name == "W":
             r = run_worker(fac, 100000, 62500, args.steps, args.cpu_seconds, args.threads)
         else:
