@@ -98,11 +98,15 @@ __global__ void __launch_bounds__(256, 4) k_sha512_many(uint32_t n, const uint8_
 
 // ------------------------------------------------------------------------------------ schedule / round split
 static constexpr uint32_t SPLIT_MAX_N = 32768;    // above: k_sha512_many (every SIMD has work anyway)
-// Unused dynamic LDS reserved by each k_sha512_split2 workgroup (variant builds only: with enough of
-// it no other kernel's workgroup fits on a digest workgroup's CU, tools/build_variants.sh).
-#ifndef NW_SHA_LDS_PAD
-#define NW_SHA_LDS_PAD 0
+// A digest launch that fits one workgroup per CU (n <= 32 x CUs: C4's 1,250 worker batches, a lone
+// header) reserves unused dynamic LDS so that no other kernel's workgroup (k_verify: 24 KB) fits
+// beside it: the chains then run on CUs of their own instead of sharing SIMD issue with the
+// verify waves of the same step (LDS per CU: 160 KB; the workgroup's own 63,360 B + the pad leaves
+// < 24 KB).  NW_SHA_EXCLUSIVE=0: no pad (A/B variant builds).
+#ifndef NW_SHA_EXCLUSIVE
+#define NW_SHA_EXCLUSIVE 1
 #endif
+static constexpr uint32_t SHA_EXCLUSIVE_PAD = 80000;
 
 // ------------------------------------------------------------------------------------ two-lane split
 // The rounds on lane pairs (nw_sha512_2l.h: 20 instructions per round for one message instead of
@@ -286,14 +290,22 @@ hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* o
                               uint8_t* out, hipStream_t st) {
     if (n == 0) return hipSuccess;
     if (n <= SPLIT_MAX_N) {
-        if (NW_SHA_LDS_PAD > 0) {
+        const uint32_t blocks = blocks_for(n, SPLIT2_MSGS);
+        uint32_t pad = 0;
+        if (NW_SHA_EXCLUSIVE) {
+            static const int cus = [] {
+                int dev = 0, c = 0;
+                if (hipGetDevice(&dev) != hipSuccess ||
+                    hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                    return 0;
+                return c;
+            }();
             static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sha512_split2<0>),
                                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                               NW_SHA_LDS_PAD);
-            if (attr != hipSuccess) return attr;
+                                                               (int)SHA_EXCLUSIVE_PAD);
+            if (attr == hipSuccess && blocks <= (uint32_t)cus) pad = SHA_EXCLUSIVE_PAD;
         }
-        hipLaunchKernelGGL(k_sha512_split2<0>, dim3(blocks_for(n, SPLIT2_MSGS)), dim3(192), NW_SHA_LDS_PAD, st, n, base,
-                           off, len, out);
+        hipLaunchKernelGGL(k_sha512_split2<0>, dim3(blocks), dim3(192), pad, st, n, base, off, len, out);
     } else {
         hipLaunchKernelGGL(k_sha512_many, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, base, off, len, out);
     }
