@@ -728,7 +728,6 @@ def main(argv=None):
         d_bouts = [torch.empty((ndig, 64), dtype=torch.uint8, device=dev) for _ in range(nst)]
         # one digest stream per batch in flight: step i's digests overlap step i + 1's
         s_digs = [torch.cuda.Stream(device=dev) for _ in range(nst)]
-        ev_digs = [torch.cuda.Event() for _ in range(nst)]
 
     # N > 1: every all_gather on one stream (collectives of one communicator stay serialized), after
     # its batch's kernels; a stream reuses its output set only after that set's all_gather
@@ -740,14 +739,12 @@ def main(argv=None):
         n_step[0] += 1
         cur, o = streams[i % nst], outs[i % nst]
         if ndig:
-            s_dig, ev_dig = s_digs[i % nst], ev_digs[i % nst]
-            s_dig.wait_stream(cur)
+            # the worker digests are independent of the certificates: step i's digests follow step
+            # i - 1's on the digest stream, with no wait on the verify stream, so the two streams
+            # pipeline; the timed region still ends when every step's digests and verdicts are done
             eng.sha512_many_dev(d_bdata.data_ptr(), d_boff.data_ptr(), d_blen.data_ptr(), ndig,
-                                d_bouts[i % nst].data_ptr(), s_dig.cuda_stream)
-            ev_dig.record(s_dig)
+                                d_bouts[i % nst].data_ptr(), s_digs[i % nst].cuda_stream)
         verify_step(cur, o)
-        if ndig:
-            cur.wait_event(ev_dig)
         if world > 1:
             if s_comm is None:
                 shard.allgather_verdicts(o["ok"], o["stake"], ranges)   # RCCL all_gather of bitmaps + stake
@@ -757,6 +754,7 @@ def main(argv=None):
                     shard.allgather_verdicts(o["ok"], o["stake"], ranges)
                 cur.wait_stream(s_comm)
 
+    torch.cuda.synchronize()       # inputs resident before any stream reads them
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
