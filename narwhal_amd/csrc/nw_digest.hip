@@ -127,6 +127,16 @@ static constexpr uint32_t SPLIT2_MSGS = 32;
 static constexpr uint32_t SPLIT2_COLS = SPLIT2_MSGS + 1;   // + the column of 1s
 static constexpr int SPLIT2_HALF = 48;                      // rows of the first half (16 loaded + 32 computed)
 
+// One block's K_t + W_t for the 33 columns, with rows t and t + 1 (t even) of a column adjacent: the
+// round wave reads two rounds' values with one 128-bit LDS read (40 reads per block, not 80).
+struct alignas(16) KwBlock {
+    uint64_t v[40][SPLIT2_COLS][2];
+    __device__ __forceinline__ uint64_t& at(int t, uint32_t col) { return v[t >> 1][col][t & 1]; }
+    __device__ __forceinline__ ulonglong2 pair(int t, uint32_t col) const {   // t even
+        return *reinterpret_cast<const ulonglong2*>(&v[t >> 1][col][0]);
+    }
+};
+
 // Block k's raw dwords, loaded ahead of use when the block is a full aligned one (else nothing).
 struct RawBlock {
     uint32_t u[32];
@@ -154,11 +164,11 @@ struct RawBlock {
 // after row t >= 16 is produced, w[t & 15] holds W_t).  Rows 16.. run as 16-row groups in a rolled
 // loop: the kernel's code (three waves' worth of it) stays well inside the instruction cache.
 template <int R0, int R1>
-__device__ __forceinline__ void split2_rows(uint64_t w[16], uint64_t (*kwb)[SPLIT2_COLS], uint32_t col) {
+__device__ __forceinline__ void split2_rows(uint64_t w[16], KwBlock& kwb, uint32_t col) {
     static_assert(R0 % 16 == 0 && R1 % 16 == 0, "16-row groups");
     if (R0 == 0) {
 #pragma unroll
-        for (int t = 0; t < 16; ++t) kwb[t][col] = w[t] + SHA512_K[t];
+        for (int t = 0; t < 16; ++t) kwb.at(t, col) = w[t] + SHA512_K[t];
     }
 #pragma nounroll
     for (int g = (R0 < 16 ? 16 : R0); g < R1; g += 16) {
@@ -168,7 +178,7 @@ __device__ __forceinline__ void split2_rows(uint64_t w[16], uint64_t (*kwb)[SPLI
             const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
             const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
             w[i] += s0 + w[(i + 9) & 15] + s1;
-            kwb[g + i][col] = w[i] + SHA512_K[g + i];
+            kwb.at(g + i, col) = w[i] + SHA512_K[g + i];
         }
     }
 }
@@ -179,7 +189,7 @@ __device__ __forceinline__ void split2_rows(uint64_t w[16], uint64_t (*kwb)[SPLI
 template <int PROBE = 0>
 __global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t* base, const uint64_t* off,
                                                        const uint64_t* len, uint8_t* out) {
-    __shared__ uint64_t kw[3][80][SPLIT2_COLS];   // 63,360 B: two workgroups per CU
+    __shared__ KwBlock kw[3];                      // 63,360 B: two workgroups per CU
     const uint32_t wave = threadIdx.x >> 6;         // 0: rounds, 1: schedule A, 2: schedule B
     const uint32_t lane = threadIdx.x & 63u;
     const bool odd = lane & 1u;
@@ -205,7 +215,7 @@ __global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t
         // the round wave is the chain's critical path: when it shares a SIMD with a schedule wave, the
         // arbiter should pick it first
         __builtin_amdgcn_s_setprio(3);
-        for (uint32_t t = lane; t < 3 * 80; t += 64) kw[t / 80][t % 80][SPLIT2_MSGS] = 1ull;
+        for (uint32_t t = lane; t < 3 * 80; t += 64) kw[t / 80].at(t % 80, SPLIT2_MSGS) = 1ull;
         uint64_t h[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) h[k] = SHA512_IV[(odd ? 0 : 4) + k];
@@ -221,8 +231,8 @@ __global__ void __launch_bounds__(192) k_sha512_split2(uint32_t n, const uint8_t
         uint64_t twait = 0;
         for (uint32_t b = 0; b < nbmax; ++b) {
             if (b < nb && PROBE != 2) {
-                const uint64_t (*kb)[SPLIT2_COLS] = kw[b % 3];
-                c.block(h, [&](int t) { return kb[t][col]; });
+                const KwBlock& kb = kw[b % 3];
+                c.block<true>(h, [&](int t) { return kb.pair(t, col); });
             }
             if (PROBE == 3) {
                 const uint64_t tb = __builtin_amdgcn_s_memtime();

@@ -74,39 +74,63 @@ struct Sha2L {
 
     // K_t + W_t is read KW_AHEAD steps before its use into a register ring: a read issued in the
     // step that consumes it exposes the whole LDS latency (~50-120 cycles on a 20-instruction step)
-    // to the chain once per round.
+    // to the chain once per round.  PAIRED: kw(t) for even t returns (K_t + W_t, K_{t+1} + W_{t+1})
+    // from one 128-bit LDS read, refilling two ring slots every other step (half the reads; the ring
+    // holds two more entries so a refill never overwrites a value not yet consumed).
     static constexpr int KW_AHEAD = 4;
+    static_assert(KW_AHEAD % 2 == 0, "paired reads start on even rounds");
+    template <bool PAIRED>
+    static constexpr int ring() { return PAIRED ? KW_AHEAD + 2 : KW_AHEAD; }
 
     // step T of a block on the register array x (the roles rotate with period 4; T is a
     // compile-time constant so every index below is a fixed register)
-    template <int T, class KW>
-    __device__ __forceinline__ void block_step(uint64_t x[4], const uint64_t h[4], uint64_t q[KW_AHEAD], KW& kw) const {
+    template <int T, bool PAIRED, class KW>
+    __device__ __forceinline__ void block_step(uint64_t x[4], const uint64_t h[4], uint64_t* q, KW& kw) const {
+        constexpr int RING = ring<PAIRED>();
         uint64_t& D = x[(7 - T) & 3];
         // steps 80, 81: the even lane's result is discarded, the odd lane's kw must still be 1:
         // they reuse K_79 + W_79's slot, which is never refilled
-        const uint64_t k = q[(T < 80 ? T : 79) % KW_AHEAD];
-        if constexpr (T + KW_AHEAD < 80) q[T % KW_AHEAD] = kw(T + KW_AHEAD);
+        const uint64_t k = q[(T < 80 ? T : 79) % RING];
+        if constexpr (PAIRED) {
+            if constexpr ((T & 1) == 0 && T + KW_AHEAD < 80) {
+                const auto pr = kw(T + KW_AHEAD);
+                q[(T + KW_AHEAD) % RING] = pr.x;
+                q[(T + KW_AHEAD + 1) % RING] = pr.y;
+            }
+        } else {
+            if constexpr (T + KW_AHEAD < 80) q[T % RING] = kw(T + KW_AHEAD);
+        }
         uint64_t nv = step(x[(4 - T) & 3], x[(5 - T) & 3], x[(6 - T) & 3], D, k);
         if (T == 0) nv = sel64(m, h[1], nv);           // odd: a_{-1} = b
         else if (T == 1) nv = sel64(m, h[0], nv);      // odd: a_0 = a
         else if (T >= 80) nv = sel64(m, nv, D);        // even: keep e..h
         D = nv;
-        if constexpr (T + 1 < 82) block_step<T + 1>(x, h, q, kw);
+        if constexpr (T + 1 < 82) block_step<T + 1, PAIRED>(x, h, q, kw);
     }
 
     // One compression.  h = this lane's half of the chaining state (even: e f g h, odd: a b c d);
-    // kw(t) = K_t + W_t on the even lane and 1 on the odd lane, t = 0..79.
-    template <class KW>
+    // kw(t) = K_t + W_t on the even lane and 1 on the odd lane, t = 0..79 (PAIRED: rounds t, t + 1
+    // for even t, as a ulonglong2).
+    template <bool PAIRED = false, class KW>
     __device__ __forceinline__ void block(uint64_t h[4], KW kw) const {
-        uint64_t q[KW_AHEAD];
+        uint64_t q[ring<PAIRED>()];
+        if constexpr (PAIRED) {
 #pragma unroll
-        for (int t = 0; t < KW_AHEAD; ++t) q[t] = kw(t);
+            for (int t = 0; t < KW_AHEAD; t += 2) {
+                const auto pr = kw(t);
+                q[t] = pr.x;
+                q[t + 1] = pr.y;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < KW_AHEAD; ++t) q[t] = kw(t);
+        }
         uint64_t x[4];
         x[0] = sel64(m, h[2], h[0]);   // newest: e (even) / a_{-2} = c (odd)
         x[1] = sel64(m, h[3], h[1]);   // f / a_{-3} = d
         x[2] = h[2];                   // g / (unused)
         x[3] = h[3];                   // h / (unused)
-        block_step<0>(x, h, q, kw);
+        block_step<0, PAIRED>(x, h, q, kw);
         // even: (e f g h) = x[0] x[1] x[2] x[3];  odd: (a b c d) = x[2] x[3] x[0] x[1]
         h[0] += sel64(m, x[2], x[0]);
         h[1] += sel64(m, x[3], x[1]);

@@ -156,6 +156,27 @@ static void host_rounds(uint32_t nb, const uint64_t* kw, uint64_t st[8]) {
 }
 
 
+// The row-major K+W layout (kw[t][col], one 64-bit read per round) that k_split2_x below was written
+// against; the shipped kernel now pairs rows (KwBlock in nw_digest.hip).
+template <int R0, int R1>
+__device__ __forceinline__ void split2_rows_rm(uint64_t w[16], uint64_t (*kwb)[SPLIT2_COLS], uint32_t col) {
+    if (R0 == 0) {
+#pragma unroll
+        for (int t = 0; t < 16; ++t) kwb[t][col] = w[t] + SHA512_K[t];
+    }
+#pragma nounroll
+    for (int g = (R0 < 16 ? 16 : R0); g < R1; g += 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint64_t w15 = w[(i + 1) & 15], w2 = w[(i + 14) & 15];
+            const uint64_t s0 = xor3_64(rotr64(w15, 1), rotr64(w15, 8), w15 >> 7);
+            const uint64_t s1 = xor3_64(rotr64(w2, 19), rotr64(w2, 61), w2 >> 6);
+            w[i] += s0 + w[(i + 9) & 15] + s1;
+            kwb[g + i][col] = w[i] + SHA512_K[g + i];
+        }
+    }
+}
+
 // Variants of k_sha512_split2 (same code, stamps added) to find what couples the round wave to
 // its placement.  MODE 0: as shipped; 1: the round wave reads K+W from a private LDS copy filled
 // once (the schedule waves still run and write kw); 2: the schedule waves use synthetic block
@@ -260,8 +281,8 @@ __global__ void __launch_bounds__(192) k_split2_x(uint32_t n, const uint8_t* bas
             sha512_load_block(m, L, k0, w);
             rb.issue(m, L, k0 + 2, nb);
         }
-        split2_rows<0, SPLIT2_HALF>(w, kw[k0 % 3], j);
-        if (par == 0) split2_rows<SPLIT2_HALF, 80>(w, kw[k0 % 3], j);
+        split2_rows_rm<0, SPLIT2_HALF>(w, kw[k0 % 3], j);
+        if (par == 0) split2_rows_rm<SPLIT2_HALF, 80>(w, kw[k0 % 3], j);
     }
     __syncthreads();
     uint64_t busy = 0;
@@ -273,11 +294,11 @@ __global__ void __launch_bounds__(192) k_split2_x(uint32_t n, const uint8_t* bas
                 if (k < nb) {
                     words(k);
                     if (MODE != 2) rb.issue(m, L, k + 2, nb);
-                    split2_rows<0, SPLIT2_HALF>(w, kw[k % 3], j);
+                    split2_rows_rm<0, SPLIT2_HALF>(w, kw[k % 3], j);
                 }
             } else {
                 const uint32_t k = p + 1;
-                if (k < nb) split2_rows<SPLIT2_HALF, 80>(w, kw[k % 3], j);
+                if (k < nb) split2_rows_rm<SPLIT2_HALF, 80>(w, kw[k % 3], j);
             }
         }
         busy += __builtin_amdgcn_s_memtime() - ts;
