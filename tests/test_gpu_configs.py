@@ -1,11 +1,11 @@
 """GPU parity at every BASELINE.json config, on the committee-mode engine the
-bench and the Rust shim use (key_window = -1: W20 at 100 keys, W16 at 1,000, W12 at 10,000).
+bench and the Rust shim use (key_window = -1: W20 at 100 keys, W16 at 1,000, W13 at 10,000).
 
   C2  100 validators, 14,926 certificates x 67 votes (1,000,042 sigs): the benchmarked W20 kernel
   C3  1,000 validators, one round of 1,000 certificates x 667 votes: every certificate vs the oracle
   C5  C3 with 1% adversarial signatures (tests/adversarial_mix.py): every certificate verdict and
       every adversarial strict verdict vs the oracle
-  C4  10,000 validators, one GPU's share of a round (1,250 certificates x 6,667 votes, W12)
+  C4  10,000 validators, one GPU's share of a round (1,250 certificates x 6,667 votes, W13)
   W   worker batch digests (worker/src/processor.rs:65): 508,052-B and 1,000,012-B batches
 
 The checker is oracle/nw_ref.c (C restatement of dalek 1.0.1's verify_batch / verify_strict),
@@ -219,7 +219,7 @@ def test_c4_w12_sample_vs_oracle_and_localized():
     eng = _engine()
     try:
         com, slots, cs = _setup(eng, 10000, 1250, 6667)
-        assert eng.key_window() == 12 and cs.nsigs == 1250 * 6667
+        assert eng.key_window() == 13 and cs.nsigs == 1250 * 6667
         rng = np.random.default_rng(9)
         bad = rng.choice(cs.nsigs, 40, replace=False)
         sigs = cs.sigs
