@@ -743,7 +743,9 @@ def main(argv=None):
             # launched before the step's verify kernels, so the digest workgroups get their (exclusive)
             # CUs first; the step ends when both are done.  (Not joining the streams per step, so
             # that step i + 1's digests start while step i verifies, measured slower: 414-437 vs
-            # 486-491 M sigs/s, r04r: a digest launched while k_verify holds every CU waits for CUs.)
+            # 486-491 M sigs/s, r04r: a digest launched while k_verify holds every CU waits for CUs;
+            # two alternating digest streams without the join, 460 M, r04u: the second stream's digest
+            # still started only when the first finished, then waited for CUs.)
             s_dig, ev_dig = s_digs[i % nst], ev_digs[i % nst]
             s_dig.wait_stream(cur)
             eng.sha512_many_dev(d_bdata.data_ptr(), d_boff.data_ptr(), d_blen.data_ptr(), ndig,
