@@ -378,7 +378,10 @@ int grow_keys(nw_ctx* ctx, size_t need) {
         set_error(ctx, "key cache capacity exceeded (nw_opts.max_keys)");
         return NW_ERR_NOMEM;
     }
-    size_t cap = ctx->key_cap ? ctx->key_cap : 64;
+    // The first load sizes the cache to its keys (rounded up to 64): in committee mode it IS the
+    // committee, and doubling from 64 would reserve up to 2x the tables (16,384 W13 tables = 172 GB
+    // for a 10,000-key committee, against 105 GB used).  Later loads grow it by doubling.
+    size_t cap = ctx->key_cap ? ctx->key_cap : (need + 63) / 64 * 64;
     while (cap < need) cap *= 2;
     if (cap > ctx->max_keys) cap = ctx->max_keys;
     uint32_t *raw = nullptr, *info = nullptr, *stake = nullptr, *tab = nullptr;
@@ -720,12 +723,7 @@ public:
     hipError_t copy(void* dst, const uint8_t* h, size_t n) {
         return n ? hipMemcpyAsync(dst, h, n, hipMemcpyHostToDevice, st_) : hipSuccess;
     }
-    hipError_t put(void* dst, const void* src, size_t n) {
-        if (!n) return hipSuccess;
-        uint8_t* h = alloc(n);
-        std::memcpy(h, src, n);
-        return copy(dst, h, n);
-    }
+    hipError_t put(void* dst, const void* src, size_t n);
 
 private:
     Workspace* ws_;
@@ -737,15 +735,20 @@ private:
 // as soon as it is staged, so the DMA of one chunk overlaps the memcpy of the next.
 constexpr size_t kStageChunk = 4u << 20;
 
-// Large uploads (a window of worker batches is ~640 MB) are staged by several threads: one thread's
-// memcpy into pinned memory runs at ~22 GB/s on the box's EPYC host, below the ~55 GB/s PCIe DMA
-// behind it.  Chunk c covers staging bytes [cb[c], cb[c+1]); copy_chunk(c) fills it.  Helper
-// threads and the calling thread take chunks from a shared counter, and the calling thread issues
-// the DMAs strictly in chunk order, each as soon as its chunk is staged, so the uploads still
-// overlap the staging.  Helpers are started per call (tens of microseconds against milliseconds
-// of copying); below kStageParallelMin bytes everything stays on the calling thread.
+// Large uploads (a window of worker batches is ~640 MB) are staged by several threads: one thread's memcpy into pinned memory runs at ~22 GB/s on the
+// box's EPYC host, below the ~55 GB/s PCIe DMA behind it.  Chunk c covers staging bytes
+// [cb[c], cb[c+1]); copy_chunk(c) fills it.  Helper threads and the calling thread take chunks from
+// a shared counter, and the calling thread issues the DMAs strictly in chunk order, each as soon as
+// its chunk is staged, so the uploads still overlap the staging.  Helpers are started per call
+// (tens of microseconds against milliseconds of copying), at most kMaxStageHelpers across all
+// concurrent calls (host-buffer calls from many threads must not oversubscribe the host); below
+// kStageParallelMin bytes everything stays on the calling thread.  (Helpers from 2 MiB up, with
+// 1 MiB chunks, left the uncached-key call unchanged (50.2 M sigs/s) and measured the worker
+// digest windows slower on the same run, r04v.)
 constexpr size_t kStageParallelMin = 32u << 20;
-constexpr unsigned kStageThreads = 8;   // including the calling thread; the box's cgroup quota is 16 CPUs
+constexpr unsigned kStageThreads = 8;           // per call, including the calling thread
+constexpr int kMaxStageHelpers = 8;             // across calls; the box's cgroup quota is 16 CPUs
+std::atomic<int> g_stage_helpers{0};
 
 template <class CopyChunk>
 hipError_t stage_chunks(size_t nch, const size_t* cb, CopyChunk&& copy_chunk, const uint8_t* h, uint8_t* d,
@@ -753,7 +756,17 @@ hipError_t stage_chunks(size_t nch, const size_t* cb, CopyChunk&& copy_chunk, co
     auto dma = [&](size_t c) {
         return hipMemcpyAsync(d + cb[c], h + cb[c], cb[c + 1] - cb[c], hipMemcpyHostToDevice, st);
     };
-    const size_t helpers = cb[nch] - cb[0] >= kStageParallelMin ? std::min<size_t>(kStageThreads - 1, nch / 2) : 0;
+    size_t want = cb[nch] - cb[0] >= kStageParallelMin ? std::min<size_t>(kStageThreads - 1, nch / 2) : 0;
+    size_t helpers = 0;
+    while (helpers < want) {   // reserve helper slots from the process-wide cap
+        int cur = g_stage_helpers.load(std::memory_order_relaxed);
+        if (cur >= kMaxStageHelpers) break;
+        if (g_stage_helpers.compare_exchange_weak(cur, cur + 1, std::memory_order_relaxed)) ++helpers;
+    }
+    struct Release {
+        size_t n;
+        ~Release() { if (n) g_stage_helpers.fetch_sub((int)n, std::memory_order_relaxed); }
+    } release{helpers};
     if (helpers == 0) {
         for (size_t c = 0; c < nch; ++c) {
             copy_chunk(c);
@@ -773,6 +786,7 @@ hipError_t stage_chunks(size_t nch, const size_t* cb, CopyChunk&& copy_chunk, co
         return true;
     };
     std::vector<std::thread> pool;
+    pool.reserve(helpers);
     for (size_t t = 0; t < helpers; ++t) {
         try {
             pool.emplace_back([&] { while (take()) {} });
@@ -801,6 +815,14 @@ hipError_t staged_h2d(uint8_t* h, uint8_t* dst, const uint8_t* src, size_t n, hi
     cb[nch] = n;
     return stage_chunks(nch, cb.data(), [&](size_t c) { std::memcpy(h + cb[c], src + cb[c], cb[c + 1] - cb[c]); },
                         h, dst, st);
+}
+
+hipError_t Stager::put(void* dst, const void* src, size_t n) {
+    if (!n) return hipSuccess;
+    uint8_t* h = alloc(n);
+    if (n >= kStageParallelMin) return staged_h2d(h, static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), n, st_);
+    std::memcpy(h, src, n);
+    return copy(dst, h, n);
 }
 
 size_t message_bytes(const size_t* len, size_t n) {
