@@ -227,7 +227,11 @@ int fail(nw_ctx* c, hipError_t e, const char* what) {
 // only a full pool falls back to the most recently freed workspace and its completion event.
 class Lease {
 public:
-    explicit Lease(nw_ctx* ctx, hipStream_t st = nullptr) : ctx_(ctx) {
+    // pinned_hint: bytes of pinned staging the call will need; an idle workspace that already has
+    // them is preferred (growing a pinned buffer costs ~0.1 s per GB of pinning, and the first DMAs
+    // from new pinned pages stall: a 1,250-batch worker window on a workspace grown mid-run ran at
+    // half the rate, r04w).
+    explicit Lease(nw_ctx* ctx, hipStream_t st = nullptr, size_t pinned_hint = 0) : ctx_(ctx) {
         std::unique_lock<std::mutex> g(ctx->pool_mu);
         for (;;) {
             auto& fr = ctx->free_ws;
@@ -235,8 +239,12 @@ public:
                 size_t pick = fr.size();
                 for (size_t i = fr.size(); i-- > 0 && pick == fr.size();)
                     if (fr[i]->pending && st && fr[i]->last == st) pick = i;
+                auto idle = [&](size_t i) { return !fr[i]->pending || hipEventQuery(fr[i]->done) == hipSuccess; };
+                if (pinned_hint)
+                    for (size_t i = fr.size(); i-- > 0 && pick == fr.size();)
+                        if (fr[i]->h_io.cap >= pinned_hint && idle(i)) pick = i;
                 for (size_t i = fr.size(); i-- > 0 && pick == fr.size();)
-                    if (!fr[i]->pending || hipEventQuery(fr[i]->done) == hipSuccess) pick = i;
+                    if (idle(i)) pick = i;
                 if (pick == fr.size() && ctx->pool.size() < kMaxWorkspaces) break;   // all busy: a new one
                 if (pick == fr.size()) pick = fr.size() - 1;
                 ws_ = fr[pick];
@@ -1636,12 +1644,12 @@ int nw_sha512_many_async(nw_ctx* ctx, const uint8_t* const* msg, const size_t* l
         off[i] = total;
         total += (len[i] + 15) & ~(size_t)15;
     }
-    j->lease = std::make_unique<Lease>(ctx);
+    const size_t o_off = 0, o_len = align256(n * 8), o_msg = o_len + align256(n * 8), o_out = o_msg + align256(total);
+    j->lease = std::make_unique<Lease>(ctx, nullptr, o_out + n * 64);
     Workspace* ws = j->lease->ws();
     if (!ws) return NW_ERR_DEVICE;
     hipStream_t st = ws->stream;
     NW_TRY(j->lease->bind(st, true), "hipStreamWaitEvent");
-    const size_t o_off = 0, o_len = align256(n * 8), o_msg = o_len + align256(n * 8), o_out = o_msg + align256(total);
     j->o_out = o_out;
     NW_TRY(ws->h_io.ensure(o_out + n * 64), "pinned io");
     NW_TRY(ws->ensure(ws->w_msg, total + 16), "ws msg");

@@ -1,6 +1,6 @@
 set -o pipefail
 OUT=gpurun_out/${1:-r04w}; mkdir -p $OUT; export TMPDIR=/tmp
-for v in def noexcl def2; do
+for v in def def2 def3; do
   L=""; [ $v = noexcl ] && L=$PWD/build_exp/libnwcrypto_noexcl.so
   NWCRYPTO_LIB=$L timeout -k 10 300 python3 -u tools/worker_leg.py > $OUT/worker_$v.json 2> $OUT/worker_$v.err || { echo "WORKER $v FAILED"; tail -20 $OUT/worker_$v.err; exit 1; }
   python3 -c "
