@@ -23,6 +23,8 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--bench", help="bench.py JSON line of the same build (key window, sigs/launch, live frac)")
     ap.add_argument("--skip", type=int, default=2, help="warm-up launches to drop")
+    ap.add_argument("--take", type=int, default=0, help="launches to use after the skipped ones (0: all; bench.py's "
+                                                          "timed region is followed by 3 isolated launches)")
     ap.add_argument("--sigs", type=float, default=1000042.0, help="signatures per k_verify launch")
     ap.add_argument("--key-window", type=int, default=20)
     ap.add_argument("--base-window", type=int, default=24)
@@ -40,7 +42,7 @@ def main():
             b = json.loads([ln for ln in f if ln.startswith("{")][-1])
         live = b["roofline"]
         kw = b["config"]["key_window"]
-    kept = durs[a.skip:]
+    kept = durs[a.skip:a.skip + a.take] if a.take else durs[a.skip:]
     mean = sum(kept) / len(kept)
     fm = bench.kverify_fm_per_sig(kw, bw)
     peak = bench.valu_peak_mad_per_s()
@@ -52,6 +54,8 @@ def main():
     if live:
         out["frac_live_events"] = live["frac"]
         out["avg_launch_ms_live"] = live["avg_launch_ms"]
+        if live.get("isolated"):
+            out["isolated_live"] = live["isolated"]
         out["rocprof_vs_live"] = out["frac_rocprof"] / live["frac"]
     print(json.dumps(out))
 
