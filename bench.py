@@ -484,7 +484,7 @@ def launch_ranks(args, argv):
 # the node's round, partitioned over the ranks by shard.partition (strong scaling: C3 =
 # configs[2], 1,000 certificates x 667 votes; config/src/lib.rs:189-194 gives the 2f+1 = 667).
 CONFIGS = {
-    "C2": {"validators": 100, "certs": 14926, "votes": 67, "scope": "rank", "digest_batches": 0, "streams": 2,
+    "C2": {"validators": 100, "certs": 14926, "votes": 67, "scope": "rank", "digest_batches": 0, "streams": 1,
            "baseline": "configs[1]: 100-validator committee, 67-vote certificates, 1M signatures per MI355X"},
     "C3": {"validators": 1000, "certs": 1000, "votes": 667, "scope": "node", "digest_batches": 0, "streams": 2,
            "baseline": "configs[2]: 1,000-validator committee, 667-vote certificates, sharded over the GPUs "
@@ -514,8 +514,10 @@ def parse_args(argv):
     ap.add_argument("--streams", type=int, default=None,
                     help="batches in flight: step i runs on stream i mod S with its own output buffers, so one "
                          "batch's k_finish / slow path overlaps the next batch's k_verify (1: strictly serial). "
-                         "Default per config: 2 for C2 / C3; 1 for C4, where two 8.3M-signature k_verify launches "
-                         "over 10,000 key tables slow each other down (r04o: 401 vs 466 M sigs/s)")
+                         "Default per config: 2 for C3 (+11%%, r04n); 1 for C2, where two in flight gain 1.6%% "
+                         "(r04p) but the timed k_verify launches then overlap each other and the roofline "
+                         "measures shared time (frac 0.40-0.45 instead of ~0.47); 1 for C4, where two 8.3M-signature "
+                         "k_verify launches over 10,000 key tables slow each other down (r04o: 401 vs 466 M sigs/s)")
     ap.add_argument("--key-window", type=int, default=-1,
                     help="key comb window; -1 = committee mode (library sizes it for the loaded committee)")
     ap.add_argument("--dry-run", action="store_true",
@@ -802,10 +804,10 @@ def main(argv=None):
     value = total_sigs / elapsed
 
     iso = None
-    if rank == 0 and nst > 1:
-        # k_verify alone (one batch at a time, after the timed region): with batches in flight the
-        # timed launches share the SIMDs with the other batch's kernels, so their durations are longer
-        # than the kernel's own
+    if rank == 0:
+        # k_verify alone (after the timed region, the GPU idle between launches): the timed launches
+        # run back to back (and, with batches in flight, beside the other batch's kernels), so their
+        # durations include the clock the chip holds under sustained load
         eng.profile_enable(True)
         for _ in range(3):
             verify_step(streams[0], outs[0])
@@ -834,8 +836,9 @@ def main(argv=None):
             "isolated": None if not iso or not iso[1] else {
                 "avg_launch_ms": iso[0] / iso[1], "launches": iso[1],
                 "frac": sigs_per_launch * fm * MADS_PER_FM / (iso[0] / iso[1] / 1e3) / 1e12 / peak,
-                "note": "k_verify launched alone after the timed region (frac above: the timed launches, which "
-                        "overlap the other batch's k_finish / preamble)"},
+                "note": "k_verify launched alone after the timed region, the GPU idle between launches (frac "
+                        "above: the timed launches, back to back%s)" % (
+                            ", overlapping the other batch's kernels" if nst > 1 else "")},
             "work_model": "%.0f sigs/launch (%d launches per step) x %d FM/sig (7 FM per mixed addition x (%d basepoint "
                           "+ %d key - 1) comb positions + 1 FM for the chain's first entry, key window %d) x 100 u32 "
                           "MADs; SHA-512/mod-l/recoding VALU work not counted; peak = measured v_mad_u64_u32 rate"
