@@ -82,3 +82,23 @@ def test_async_abi_poll_and_out_of_order_wait(engine):
     assert j2.wait() == [hashlib.sha512(m).digest() for m in (b"abc", b"", bytes(200))]
     d1 = j1.wait()
     assert d1 == [hashlib.sha512(big[i].tobytes()).digest() for i in range(64)]
+
+
+def test_async_window_above_parallel_staging_threshold(engine):
+    """A window of ~46 MB (above the 32 MiB threshold where nw_sha512_many_async packs with helper
+    threads, chunk DMAs issued in order as chunks complete): odd lengths, unaligned sources and
+    empty messages at chunk edges all hash like hashlib."""
+    rng = np.random.default_rng(11)
+    raw = bytes(rng.integers(0, 256, 600_000, dtype=np.uint8))
+    msgs = []
+    for i in range(90):
+        if i % 9 == 4:
+            msgs.append(b"")
+        elif i % 3 == 0:
+            o = 1 + i % 13
+            msgs.append(memoryview(raw)[o:o + 508_052 + 3 * i])
+        else:
+            msgs.append(bytes(rng.integers(0, 256, 508_000 + 17 * i, dtype=np.uint8)))
+    assert sum(len(m) for m in msgs) > 40 << 20
+    got = engine.sha512_many_submit(msgs).wait()
+    assert got == [hashlib.sha512(bytes(m)).digest() for m in msgs]
