@@ -98,15 +98,19 @@ __global__ void __launch_bounds__(256, 4) k_sha512_many(uint32_t n, const uint8_
 
 // ------------------------------------------------------------------------------------ schedule / round split
 static constexpr uint32_t SPLIT_MAX_N = 32768;    // above: k_sha512_many (every SIMD has work anyway)
-// A digest launch that fits one workgroup per CU (n <= 32 x CUs: C4's 1,250 worker batches, a lone
-// header) reserves unused dynamic LDS so that no other kernel's workgroup (k_verify: 24 KB) fits
-// beside it: the chains then run on CUs of their own instead of sharing SIMD issue with the
-// verify waves of the same step (LDS per CU: 160 KB; the workgroup's own 63,360 B + the pad leaves
-// < 24 KB).  NW_SHA_EXCLUSIVE=0: no pad (A/B variant builds).
+// A digest launch of SHA_EXCLUSIVE_MIN_WG or more workgroups that still fits one per CU
+// (225 <= n <= 32 x CUs: C4's 1,250 worker batches, a worker window) reserves unused dynamic LDS so
+// that no other kernel's workgroup (k_verify: 24 KB) fits beside it: the chains then run on CUs of
+// their own instead of sharing SIMD issue with the verify waves of the same step (LDS per CU:
+// 160 KB; the workgroup's own 63,360 B + the pad leaves < 24 KB).  The price: such a workgroup
+// needs an EMPTY CU, which a running k_verify (its dispatcher refilling every freed slot) may not
+// leave until it drains, so a lone header's digest (one workgroup, latency-critical) stays unpadded.
+// NW_SHA_EXCLUSIVE=0: no pad (A/B variant builds).
 #ifndef NW_SHA_EXCLUSIVE
 #define NW_SHA_EXCLUSIVE 1
 #endif
 static constexpr uint32_t SHA_EXCLUSIVE_PAD = 80000;
+static constexpr uint32_t SHA_EXCLUSIVE_MIN_WG = 8;
 
 // ------------------------------------------------------------------------------------ two-lane split
 // The rounds on lane pairs (nw_sha512_2l.h: 20 instructions per round for one message instead of
@@ -313,7 +317,8 @@ hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* o
             static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_sha512_split2<0>),
                                                                hipFuncAttributeMaxDynamicSharedMemorySize,
                                                                (int)SHA_EXCLUSIVE_PAD);
-            if (attr == hipSuccess && blocks <= (uint32_t)cus) pad = SHA_EXCLUSIVE_PAD;
+            if (attr == hipSuccess && blocks >= SHA_EXCLUSIVE_MIN_WG && blocks <= (uint32_t)cus)
+                pad = SHA_EXCLUSIVE_PAD;
         }
         hipLaunchKernelGGL(k_sha512_split2<0>, dim3(blocks), dim3(192), pad, st, n, base, off, len, out);
     } else {
