@@ -486,7 +486,7 @@ def launch_ranks(args, argv):
 CONFIGS = {
     "C2": {"validators": 100, "certs": 14926, "votes": 67, "scope": "rank", "digest_batches": 0, "streams": 1,
            "baseline": "configs[1]: 100-validator committee, 67-vote certificates, 1M signatures per MI355X"},
-    "C3": {"validators": 1000, "certs": 1000, "votes": 667, "scope": "node", "digest_batches": 0, "streams": 2,
+    "C3": {"validators": 1000, "certs": 1000, "votes": 667, "scope": "node", "digest_batches": 0, "streams": 3,
            "baseline": "configs[2]: 1,000-validator committee, 667-vote certificates, sharded over the GPUs "
                        "with an RCCL verdict all-gather"},
     "C4": {"validators": 10000, "certs": 1250, "votes": 6667, "scope": "rank", "digest_batches": 1250, "streams": 1,
@@ -514,7 +514,7 @@ def parse_args(argv):
     ap.add_argument("--streams", type=int, default=None,
                     help="batches in flight: step i runs on stream i mod S with its own output buffers, so one "
                          "batch's k_finish / slow path overlaps the next batch's k_verify (1: strictly serial). "
-                         "Default per config: 2 for C3 (+11%%, r04n); 1 for C2, where two in flight gain 1.6%% "
+                         "Default per config: 3 for C3 (+14%% over one, r04cc); 1 for C2, where two in flight gain 1.6%% "
                          "(r04p) but the timed k_verify launches then overlap each other and the roofline "
                          "measures shared time (frac 0.40-0.45 instead of ~0.47); 1 for C4, where two 8.3M-signature "
                          "k_verify launches over 10,000 key tables slow each other down (r04o: 401 vs 466 M sigs/s)")

@@ -20,10 +20,14 @@ static constexpr uint32_t SK_SKIP = 0;            // certificate already rejecte
 static constexpr uint32_t SK_SMALL = 1;           // D_i of small order (or z_i = 0): record = (z_i mod 8) D_i
 static constexpr uint32_t SK_BIG = 2;             // D_i has a prime-order component and z_i != 0
 static constexpr uint32_t SK_MUL = 3;             // SK_BIG whose z_i D_i was computed (record holds z_i D_i)
-// Per-certificate exact-path state word: the number of SK_BIG entries, and a flag set as soon as
-// the certificate is known to be rejected (a vote with bad S / undecodable A / undecodable R).
+// Per-certificate exact-path state word: the number of SK_BIG entries and two rejection flags.
+// CS_DOOM: a vote with bad S / undecodable A (set by k_finish, so final before k_slow_prep, which
+// skips such certificates' entries).  CS_RDOOM: a vote whose R failed to decode (set by k_slow_prep
+// itself; k_slow_prep does NOT skip on it, so every slow entry of a certificate not doomed by
+// k_finish decodes its own R and NW_F_R_BAD is the same on every run; k_slow_mul skips both).
 static constexpr uint32_t CS_DOOM = 0x80000000u;
-static constexpr uint32_t CS_BIG_MASK = 0x7FFFFFFFu;
+static constexpr uint32_t CS_RDOOM = 0x40000000u;
+static constexpr uint32_t CS_BIG_MASK = 0x3FFFFFFFu;
 // internal flag bit: k_verify parked P_i (extended) in pslow[i] (its y did not match R's); cleared
 // by k_slow_prep before the flags reach the caller (every such signature is on the slow list)
 static constexpr uint32_t NW_F_P_SAVED = 0x4000u;

@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(256) k_slow_mul(VerifyParams a) {
         const uint32_t i = a.slow_list[t];
         const uint32_t cert = a.sig_cert[i];
         const uint32_t cs = a.cert_state[cert];
-        if ((cs & CS_DOOM) || (cs & CS_BIG_MASK) < 2u) continue;
+        if ((cs & (CS_DOOM | CS_RDOOM)) || (cs & CS_BIG_MASK) < 2u) continue;
         const ge_p3 D = ge_to_vgpr(load_p3(rec));
         uint32_t z4[4];
         coeff_z(a, i, cert, z4);

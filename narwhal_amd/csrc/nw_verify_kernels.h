@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
         if (!ge_decompress(Rp, R)) {
             if (owner) {
                 a.flags[i] = (fi & ~NW_F_P_SAVED) | NW_F_R_BAD;
-                atomicOr(&a.cert_state[cert], CS_DOOM);
+                atomicOr(&a.cert_state[cert], CS_RDOOM);
                 rec[SLOW_KIND] = SK_SKIP;
             }
             continue;

@@ -195,3 +195,55 @@ def test_sha512_unaligned_padding_block_ends_flush(engine, sh):
                                torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         assert bytes(d_out[0].cpu().numpy()) == hashlib.sha512(buf[sh:].cpu().numpy().tobytes()).digest(), L
+
+
+def _undecodable_r(rng, sig):
+    """sig with R replaced by 32 bytes that do not decode (the oracle's decompress fails)."""
+    while True:
+        r = bytes(rng.randrange(256) for _ in range(32))
+        if o.decompress(r) is None:
+            return r + sig[32:]
+
+
+def test_undecodable_r_flags_are_deterministic(engine, keys):
+    """Certificates with several undecodable R's: every such vote carries NW_F_R_BAD on every run
+    (k_slow_prep decodes each slow entry of a certificate that k_finish did not reject; an R failure
+    found in the same kernel no longer makes later entries skip their decode), the certificates are
+    rejected, and two runs return identical flags."""
+    import torch
+    rng, seeds, pks, slots = keys
+    ncert, nv = 300, 7
+    msgs, sigs, bad = [], [], set()
+    for c in range(ncert):
+        m, s = _cert(rng, seeds, nv)
+        if c % 3 == 0:
+            for v in (1, 3, 5):
+                s[v] = _undecodable_r(rng, s[v])
+                bad.add(c * nv + v)
+        msgs.append(m)
+        sigs += s
+    dev = torch.device("cuda", 0)
+    d_first = torch.from_numpy(np.arange(ncert, dtype=np.int32) * nv).to(dev)
+    d_n = torch.full((ncert,), nv, dtype=torch.int32, device=dev)
+    d_sig = torch.from_numpy(np.frombuffer(b"".join(sigs), np.uint8).copy()).to(dev)
+    d_signer = torch.tensor(slots[:nv] * ncert, dtype=torch.int32, device=dev)
+    d_msg = torch.from_numpy(np.frombuffer(b"".join(msgs), np.uint8).copy()).to(dev)
+    runs = []
+    for _ in range(3):
+        ok = torch.zeros(ncert, dtype=torch.uint8, device=dev)
+        flags = torch.zeros(ncert * nv, dtype=torch.int32, device=dev)
+        st = torch.zeros(ncert, dtype=torch.int64, device=dev)
+        engine.verify_certs_dev(ncert, d_first.data_ptr(), d_n.data_ptr(), ncert * nv, d_sig.data_ptr(),
+                                d_signer.data_ptr(), d_msg.data_ptr(), ZSEED, 0, ok.data_ptr(), flags.data_ptr(),
+                                st.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        runs.append((ok.cpu().numpy().astype(bool), flags.cpu().numpy()))
+    ok0, fl0 = runs[0]
+    for okr, flr in runs[1:]:
+        assert (okr == ok0).all() and (flr == fl0).all()
+    assert ok0.tolist() == [c % 3 != 0 for c in range(ncert)]
+    r_bad = {int(i) for i in np.nonzero(fl0 & 0x2000)[0]}
+    assert r_bad == bad
+    for c in (0, 3, 1):
+        f = c * nv
+        assert bool(ok0[c]) == _expect(msgs[c], pks[:nv], sigs[f:f + nv], c)

@@ -29,7 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import numpy as np  # noqa: E402
 
 L = 2**252 + 27742317777372353535851937790883648493
-STREAMS = 2   # batches in flight (bench.py --streams); --streams overrides
+STREAMS = 3   # batches in flight (bench.py --streams; 3 vs 2: C5 545 vs 513 M, C3 685 vs 662 M, r04cc)
 
 
 def log(*a):
