@@ -8,9 +8,9 @@ threads, worker/src/processor.rs:75-79).
   NW_ERR_ARG (synchronous check) or writes NW_ERR_ARG to the status word (asynchronous), and never
   faults.
 * A NULL zseed is NW_ERR_ARG at every batch entry point.
-* One thread with batches in flight on two streams (bench.py --streams 2): calls alternate between
-  the streams with no synchronization in between, each on its own workspace, and every output set
-  equals the serial result.
+* One thread with batches in flight on three streams (bench.py --streams 3): calls alternate between
+  the streams with no synchronization in between, each on its own workspace, every output set
+  equals the serial result, and repeated calls return identical flag words.
 """
 import ctypes
 import threading
@@ -130,26 +130,29 @@ def test_concurrent_dev_host_and_uncached_calls(setup):
     assert eng.committee_size() == 40
 
 
-def test_batches_in_flight_on_two_streams(setup):
+def test_batches_in_flight_on_three_streams(setup):
     import torch
     eng, com, slots, cs, dev = setup
     d = _dev_inputs(cs, slots, dev)
-    sts = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+    sts = [torch.cuda.Stream(device=dev) for _ in range(3)]
     torch.cuda.synchronize()
-    bases = [0, 1000, 2000, 3000, 0, 1000, 2000, 3000]
+    bases = [0, 1000, 2000, 3000, 0, 1000, 2000, 3000, 0]
     outs = []
     for i, base in enumerate(bases):          # no synchronization between the calls
-        st = sts[i % 2]
+        st = sts[i % 3]
         with torch.cuda.stream(st):
             status = torch.full((1,), 99, dtype=torch.int32, device=dev)
             outs.append((base, status) + _run_dev(eng, cs, d, dev, st, base, status=status))
     torch.cuda.synchronize()
+    first_flags = {}
     for base, status, ok, flags, stake in outs:
         r = eng.verify_certs_np(cs.cert_first, cs.cert_n, cs.sigs, slots[cs.signer], cs.msgs, ZSEED, base)
         assert int(status.item()) == 0
         assert (ok.cpu().numpy() == r[0]).all()
-        assert ((flags.cpu().numpy() & 8 != 0) == r[1]).all()
+        fl = flags.cpu().numpy()
+        assert ((fl & 8 != 0) == r[1]).all()
         assert (stake.cpu().numpy() == r[2].astype(np.int64)).all()
+        assert (fl == first_flags.setdefault(base, fl)).all()   # every flag bit, run to run
 
 
 def test_dev_bad_slot_and_range_are_arg_errors(setup):
