@@ -757,11 +757,17 @@ def main(argv=None):
         if ndig:
             cur.wait_event(ev_dig)
         if world > 1:
+            # RCCL all_gathers of the verdict bitmaps + stake and (C4) of the ranks' worker digests
+            # (32 B per batch), after this step's kernels (cur has waited for the digests above)
             if s_comm is None:
-                shard.allgather_verdicts(o["ok"], o["stake"], ranges)   # RCCL all_gather of bitmaps + stake
+                if ndig:
+                    shard.allgather_digests(d_bouts[i % nst])
+                shard.allgather_verdicts(o["ok"], o["stake"], ranges)
             else:
                 s_comm.wait_stream(cur)
                 with torch.cuda.stream(s_comm):
+                    if ndig:
+                        shard.allgather_digests(d_bouts[i % nst])
                     shard.allgather_verdicts(o["ok"], o["stake"], ranges)
                 cur.wait_stream(s_comm)
 

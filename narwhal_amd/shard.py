@@ -4,8 +4,8 @@ Certificates are independent units (``Certificate::verify``, primary/src/message
 a node's batch is split into contiguous certificate ranges balanced by vote count, one per GPU
 (one process per GPU).  Coefficient streams are keyed by the *global* certificate index
 (NW-Z v1 nonce), so a shard needs nothing from the others to reproduce the single-GPU verdicts.
-The only exchange is the RCCL all-gather of the per-shard verdict bitmaps and stake tallies
-(a few KB: latency-bound, one xGMI hop).
+The only exchanges are the RCCL all-gathers of the per-shard verdict bitmaps and stake tallies
+(a few KB: latency-bound, one xGMI hop) and, at C4, of the ranks' worker-batch digests (32 B per batch).
 """
 from __future__ import annotations
 
@@ -77,6 +77,21 @@ def allgather_verdicts(ok_local, stake_local, ranges: List[Tuple[int, int]], gro
         oks.append(unpack_bits(g[:maxb], c1 - c0))
         stakes.append(g[maxb:maxb + 8 * (c1 - c0)].view(torch.int64))
     return torch.cat(oks), torch.cat(stakes)
+
+
+def allgather_digests(digests_local, group=None):
+    """All-gather the worker-batch digests of every rank ("worker digests are
+    all-gathered the same way, 32 B per batch").  ``digests_local``: uint8 [n, >= 32] on this rank (the
+    64-byte SHA-512 outputs; the reference keeps the first 32, worker/src/processor.rs:65).  Every rank
+    contributes the same n (the per-rank batch share); returns uint8 [world * n, 32] in rank order.
+    One latency-bound collective (RCCL over xGMI on GPU tensors, gloo on CPU tensors)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    local = digests_local[:, :32].contiguous()
+    out = torch.empty((world * local.shape[0], 32), dtype=torch.uint8, device=local.device)
+    dist.all_gather_into_tensor(out, local, group=group)
+    return out
 
 
 def verify_sharded(engine, cs, slots, zseed: bytes, rank: int, world: int, group=None, device=None):

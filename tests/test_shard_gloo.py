@@ -160,3 +160,35 @@ def test_verify_sharded_and_split_batch_plumbing_gloo():
     for rank, ok, st, v_ok, v_bad in res:
         assert ok == want_ok and st == want_st, rank
         assert v_ok is True and v_bad is False, rank
+
+
+def _digest_worker(rank, world, port, n, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = torch.arange(rank * n, (rank + 1) * n, dtype=torch.int64)
+    local = ((g[:, None] * 31 + torch.arange(64)[None, :] * 7) % 251).to(torch.uint8)   # [n, 64] per rank
+    out = shard.allgather_digests(local)
+    q.put((rank, out.numpy().tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allgather_digests_gloo():
+    """C4's worker digests across ranks: every rank ends with every rank's first 32
+    digest bytes per batch, in rank order."""
+    world, n = 2, 37
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_digest_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = np.arange(world * n)[:, None]
+    want = ((g * 31 + np.arange(32)[None, :] * 7) % 251).tolist()
+    for rank, got in res:
+        assert got == want, rank
