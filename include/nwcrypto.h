@@ -71,13 +71,14 @@ typedef struct nw_opts {
     int device;        /* HIP device ordinal (one process per GPU; -1 = current device) */
     uint32_t flags;    /* reserved, 0 */
     size_t max_keys;   /* key-cache capacity in keys (0 = fill a 160 GiB HBM budget) */
-    int key_window;    /* key comb window: 8, 12, 13, 16 or 20 bits.  0 = auto at the first load (16
+    int key_window;    /* key comb window: 8, 9, 12, 13, 16 or 20 bits.  0 = auto at the first load (16
                           for <= 384 keys, 12 for <= 12288 keys, else 8); -1 = committee mode: the
                           first nw_committee_load is the committee, and the widest window whose
                           tables fit the key budget with 25% headroom is used (W20 up to 157 keys,
-                          W16 up to 2,047, W13 up to 13,104: a 10,000-validator committee).  Table
-                          bytes per key: w8 0.53 MB, w12 5.77 MB, w13 10.5 MB, w16 67.1 MB,
-                          w20 872 MB; additions per signature 32 / 22 / 20 / 16 / 13.  (The
+                          W16 up to 2,047, W13 up to 13,104: a 10,000-validator committee; W12 up to 23,819;
+                          W9 up to 144,068: the worker's 100,000 keys).  Table
+                          bytes per key: w8 0.53 MB, w9 0.95 MB, w12 5.77 MB, w13 10.5 MB,
+                          w16 67.1 MB, w20 872 MB; additions per signature 32 / 29 / 22 / 20 / 16 / 13.  (The
                           basepoint comb is fixed at w24: 11 additions, 11.8 GB per context.) */
 } nw_opts;
 

@@ -365,7 +365,7 @@ constexpr size_t kGroupMinSigsPerKey = 4;
 // keys added later.  Committee mode (-1): the first load IS the committee; take the widest window
 // whose tables for it fit the key budget with 25% headroom (fewest additions per signature).
 int committee_window(size_t n, size_t budget) {
-    for (int w : {20, 16, 13, 12}) {
+    for (int w : {20, 16, 13, 12, 9}) {
         const double need = 1.25 * (double)n * (double)comb_words(w) * 4.0;
         if (need <= (double)budget) return w;
     }
@@ -1146,8 +1146,8 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     int dev = opts && opts->device >= 0 ? opts->device : -1;
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_DEVICE;
     if (dev >= ndev) return NW_ERR_ARG;
-    if (opts && opts->key_window && opts->key_window != -1 && opts->key_window != 8 && opts->key_window != 12 &&
-        opts->key_window != 13 && opts->key_window != 16 && opts->key_window != 20)
+    if (opts && opts->key_window && opts->key_window != -1 && opts->key_window != 8 && opts->key_window != 9 &&
+        opts->key_window != 12 && opts->key_window != 13 && opts->key_window != 16 && opts->key_window != 20)
         return NW_ERR_ARG;
     nw_ctx* ctx = new nw_ctx();
     ctx->device = dev;

@@ -30,6 +30,7 @@ namespace nw {
 template <int WA>
 hipError_t launch_vs_wa(const VerifyParams& p, int msgmode, bool slow, uint32_t n_upper, hipStream_t st);
 extern template hipError_t launch_vs_wa<8>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
+extern template hipError_t launch_vs_wa<9>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
 extern template hipError_t launch_vs_wa<12>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
 extern template hipError_t launch_vs_wa<13>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
 extern template hipError_t launch_vs_wa<16>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
@@ -446,6 +447,7 @@ static hipError_t launch_vs(const VerifyParams& p, int msgmode, int key_window, 
                             hipStream_t st) {
     switch (key_window) {
         case 8: return launch_vs_wa<8>(p, msgmode, slow, n_upper, st);
+        case 9: return launch_vs_wa<9>(p, msgmode, slow, n_upper, st);
         case 12: return launch_vs_wa<12>(p, msgmode, slow, n_upper, st);
         case 13: return launch_vs_wa<13>(p, msgmode, slow, n_upper, st);
         case 16: return launch_vs_wa<16>(p, msgmode, slow, n_upper, st);

@@ -68,6 +68,7 @@ hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_
     if (window == B_WINDOW) return launch_key_prep_w<B_WINDOW>(nk, keys_raw, key_info, bases, tab, st);
     switch (window) {
         case 8: return launch_key_prep_w<8>(nk, keys_raw, key_info, bases, tab, st);
+        case 9: return launch_key_prep_w<9>(nk, keys_raw, key_info, bases, tab, st);
         case 12: return launch_key_prep_w<12>(nk, keys_raw, key_info, bases, tab, st);
         case 13: return launch_key_prep_w<13>(nk, keys_raw, key_info, bases, tab, st);
         case 16: return launch_key_prep_w<16>(nk, keys_raw, key_info, bases, tab, st);

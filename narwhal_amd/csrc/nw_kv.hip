@@ -1,5 +1,5 @@
 // One key comb window's verify kernels (k_verify / k_slow_prep for both message modes).
-// Built once per window: -DNW_WA=8, 12, 13, 16, 20 (Makefile).
+// Built once per window: -DNW_WA=8, 9, 12, 13, 16, 20 (Makefile).
 #include "nw_verify_kernels.h"
 
 #ifndef NW_WA

@@ -1,5 +1,5 @@
 // One key comb window's latency-mode verify kernel (k_verify_split, both message modes).
-// Built once per window: -DNW_WA=8, 12, 13, 16, 20 (Makefile).
+// Built once per window: -DNW_WA=8, 9, 12, 13, 16, 20 (Makefile).
 #include "nw_verify_split.h"
 
 #ifndef NW_WA

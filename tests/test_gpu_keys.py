@@ -42,7 +42,7 @@ def _batch_mismatches(eng, golden):
 
 
 # ----------------------------------------------------------------------------- cached, every window
-@pytest.mark.parametrize("window", [8, 12, 13, 16, 20])
+@pytest.mark.parametrize("window", [8, 9, 12, 13, 16, 20])
 def test_cached_windows_full_golden(window, golden):
     """Every golden strict and batch verdict with all 60 golden keys in the committee cache."""
     from narwhal_amd import _lib
