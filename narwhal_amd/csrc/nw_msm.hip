@@ -84,6 +84,23 @@ NW_HD void store_niels_affine(uint32_t* dst, const ge_p3& p) {
     for (int k = 0; k < 8; ++k) q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
 
+// 64 signed nibble digits of k < 2^253 in [-8, 7], packed as 4-bit two's complement (no carry out).
+NW_HD void recode_w4(uint32_t pk[8], const uint32_t k_in[8]) {
+    int carry = 0;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+        uint32_t out = 0;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+            const int b = (int)((k_in[w] >> (4 * s)) & 15u) + carry;
+            carry = (b + 8) >> 4;
+            const int d = b - (carry << 4);
+            out |= ((uint32_t)d & 15u) << (4 * s);
+        }
+        pk[w] = out;
+    }
+}
+
 // k * Q for k < 2^253 (8 LE words): signed radix-16 digits, most significant first.  The multiples
 // 1..8 Q (projective Niels) live in this lane's 320-word slice of global scratch, so no
 // runtime-indexed register array is needed; 63 x 4 doublings (T only before an addition) and 64
@@ -98,21 +115,8 @@ NW_HD ge_p3 ge_scalarmult_w4(const uint32_t k_in[8], const ge_p3& Q, uint32_t* t
         cur = ge_add(cur, q1);
         store_cached(tab + (e - 1) * 40, ge_to_cached(cur));
     }
-    // recoding: 64 nibble digits in [-8, 7], packed as 4-bit two's complement (k < 2^253: no carry out)
     uint32_t pk[8];
-    int carry = 0;
-#pragma unroll
-    for (int w = 0; w < 8; ++w) {
-        uint32_t out = 0;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-            const int b = (int)((k_in[w] >> (4 * s)) & 15u) + carry;
-            carry = (b + 8) >> 4;
-            const int d = b - (carry << 4);
-            out |= ((uint32_t)d & 15u) << (4 * s);
-        }
-        pk[w] = out;
-    }
+    recode_w4(pk, k_in);
     ge_p3 acc = ge_identity();
 #pragma nounroll
     for (int i = 0; i < 64; ++i) {
@@ -140,17 +144,81 @@ NW_HD ge_p3 ge_scalarmult_w4(const uint32_t k_in[8], const ge_p3& Q, uint32_t* t
     return acc;
 }
 
+// ge_scalarmult_w4 with every point operation split over the 4 lanes of a quad (nw_quad.h), for a
+// strict call of at most 16 signatures, where the chain (252 doublings, 64 additions) is the
+// call's latency.  tab: the quad's LDS slice; the multiples 1..8 Q are kept as ge_add_quad_v
+// operands (entry e, lane q: tab[e * 40 + q * 10 + k]), so a lookup reads 10 words per lane.  A
+// negative digit swaps lanes 0 and 1 (Y - X <-> Y + X) and negates lane 2's T; digit 0 adds the
+// identity (operands 1, 1, 0, 1).
+__device__ ge_p3 ge_scalarmult_w4_quad(const uint32_t k_in[8], const ge_p3& Q, uint32_t* tab) {
+    const uint32_t q = threadIdx.x & 3u;
+    auto put = [&](int e, const ge_p3& p) {
+        const fe v = ge_quad_operand(p);
+#pragma unroll
+        for (int k = 0; k < 10; ++k) tab[e * 40 + q * 10 + k] = v.v[k];
+    };
+    put(0, Q);
+    ge_p3 cur = ge_dbl_quad(Q);
+    put(1, cur);
+#pragma nounroll
+    for (int e = 3; e <= 8; ++e) {
+        cur = ge_add_quad(cur, Q);
+        put(e - 1, cur);
+    }
+    __syncthreads();   // one-wave block: the quad's table writes before its lanes' lookups
+    uint32_t pk[8];
+    recode_w4(pk, k_in);
+    const fe id_op = fe_select(fe_one(), fe_zero(), q == 2u);
+    ge_p3 acc = ge_identity();
+#pragma nounroll
+    for (int i = 0; i < 64; ++i) {
+        if (i) {
+            acc = ge_dbl_quad(acc);
+            acc = ge_dbl_quad(acc);
+            acc = ge_dbl_quad(acc);
+            acc = ge_dbl_quad(acc);
+        }
+        const int d = ((int)pk[7]) >> 28;
+#pragma unroll
+        for (int w = 7; w > 0; --w) pk[w] = (pk[w] << 4) | (pk[w - 1] >> 28);
+        pk[0] <<= 4;
+        const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+        const uint32_t slot = (d < 0 && q < 2u) ? (q ^ 1u) : q;
+        const uint32_t* src = tab + (ad ? ad - 1 : 0) * 40 + slot * 10;
+        fe v;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) v.v[k] = src[k];
+        v = fe_select_mask(v, fe_carry(fe_neg(v)), lane_mask(d < 0 && q == 2u));
+        v = fe_select_mask(v, id_op, lane_mask(ad == 0));
+        acc = ge_add_quad_v(acc, v);
+    }
+    return acc;
+}
+
 // ------------------------------------------------------------------------------------ strict, uncached
 // One lane per signature (generic messages): P = s B - h A with A decompressed here and h A by
 // ge_scalarmult_w4; writes the same (X, Z, partial flags) record as k_verify, so k_finish completes
 // the strict verdict.  Semantics are those of k_verify with a cached key (nw_core.h).
-__global__ void __launch_bounds__(256) k_verify_var(VerifyParams a, uint32_t* scratch) {
-    // fewer signatures than a wave (one strict call): the idle lanes of wave 0 run duplicates, so the
-    // chain issues at the full-EXEC rate; they store only what their owner stores
-    const uint32_t graw = blockIdx.x * blockDim.x + threadIdx.x;
-    if (graw >= a.gn && (a.gn >= 64 || graw >= 64)) return;
-    const bool owner = graw < a.gn;
-    const uint32_t gid = a.g0 + (owner ? graw : graw % a.gn);
+// QUAD (at most VAR_QUAD_MAX_SIGS signatures, one 64-thread block): a quad per signature and
+// ge_scalarmult_w4_quad; quads past gn run duplicates (full EXEC) and store nothing.
+static constexpr uint32_t VAR_QUAD_MAX_SIGS = 16;
+template <bool QUAD>
+__global__ void __launch_bounds__(QUAD ? 64 : 256) k_verify_var(VerifyParams a, uint32_t* scratch) {
+    __shared__ uint32_t qtab[QUAD ? VAR_QUAD_MAX_SIGS * 320 : 1];
+    uint32_t gid;
+    bool owner;
+    if constexpr (QUAD) {
+        const uint32_t qd = threadIdx.x >> 2;
+        owner = (threadIdx.x & 3u) == 0 && qd < a.gn;
+        gid = a.g0 + qd % a.gn;
+    } else {
+        // fewer signatures than a wave (one strict call): the idle lanes of wave 0 run duplicates, so
+        // the chain issues at the full-EXEC rate; they store only what their owner stores
+        const uint32_t graw = blockIdx.x * blockDim.x + threadIdx.x;
+        if (graw >= a.gn && (a.gn >= 64 || graw >= 64)) return;
+        owner = graw < a.gn;
+        gid = a.g0 + (owner ? graw : graw % a.gn);
+    }
     const uint32_t i = gid;
     uint32_t R[8], S[8], Aw[8], h[8];
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
@@ -176,7 +244,9 @@ __global__ void __launch_bounds__(256) k_verify_var(VerifyParams a, uint32_t* sc
         zero8[k] = 0u;
     }
     ge_p3 P = comb_sB_minus_hA<B_WINDOW, 0>(s_use, zero8, a.btab, nullptr);
-    const ge_p3 hA = ge_scalarmult_w4(h, A, scratch + (size_t)gid * 320);
+    ge_p3 hA;
+    if constexpr (QUAD) hA = ge_scalarmult_w4_quad(h, A, qtab + (threadIdx.x >> 2) * 320);
+    else hA = ge_scalarmult_w4(h, A, scratch + (size_t)gid * 320);
     P = ge_add(P, ge_cached_neg(ge_to_cached(hA)));
     asm volatile("" ::: "memory");
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
@@ -554,7 +624,8 @@ hipError_t launch_msm_points_identity(uint32_t npts, const uint32_t* pts, uint8_
 hipError_t launch_verify_var(const VerifyParams& p, int msgmode, uint32_t* scratch, hipStream_t st) {
     if (p.gn == 0) return hipSuccess;
     if (msgmode != 1) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_verify_var, dim3(blocks_for(p.gn, 256)), dim3(256), 0, st, p, scratch);
+    if (p.gn <= VAR_QUAD_MAX_SIGS) hipLaunchKernelGGL(k_verify_var<true>, dim3(1), dim3(64), 0, st, p, scratch);
+    else hipLaunchKernelGGL(k_verify_var<false>, dim3(blocks_for(p.gn, 256)), dim3(256), 0, st, p, scratch);
     return hipGetLastError();
 }
 

@@ -56,11 +56,12 @@ __device__ __forceinline__ ge_p3 ge_dbl_quad(const ge_p3& p) {
 
 // a + b (both extended; the formulas of ge_add(a, ge_to_cached(b))): (Ya-Xa)(Yb-Xb),
 // (Ya+Xa)(Yb+Xb), Ta Tb, Za Zb on lanes 0..3; 2d Ta Tb on every lane; then the four products.
-__device__ __forceinline__ ge_p3 ge_add_quad(const ge_p3& a, const ge_p3& b) {
+// Here b is given as this lane's operand only (lane q: operand q of b, ge_quad_operand), so a
+// table of b's keeps 10 words per lane instead of the whole point.
+__device__ __forceinline__ ge_p3 ge_add_quad_v(const ge_p3& a, const fe& v) {
     const uint32_t q = threadIdx.x & 3u;
     const uint32_t m1 = lane_mask(q & 1u), m2 = lane_mask(q & 2u);
     const fe u = fe_quad_pick(fe_sub(a.Y, a.X), fe_add(a.Y, a.X), a.T, a.Z, m1, m2);
-    const fe v = fe_quad_pick(fe_sub(b.Y, b.X), fe_carry(fe_add(b.Y, b.X)), b.T, b.Z, m1, m2);
     const fe pr = fe_mul(u, v);
     const fe a1 = fe_quad_bcast<0>(pr), b1 = fe_quad_bcast<1>(pr), tt = fe_quad_bcast<2>(pr);
     const fe zz = fe_quad_bcast<3>(pr);
@@ -71,6 +72,17 @@ __device__ __forceinline__ ge_p3 ge_add_quad(const ge_p3& a, const ge_p3& b) {
     const fe f = fe_sub(d, c1);
     const fe g = fe_add(d, c1);
     return ge_quad_gather(fe_mul(fe_quad_pick(e, g, g, e, m1, m2), fe_quad_pick(f, h, f, h, m1, m2)));
+}
+
+// Lane q's operand of b in ge_add_quad_v: Yb - Xb, Yb + Xb (carried), Tb, Zb.
+__device__ __forceinline__ fe ge_quad_operand(const ge_p3& b) {
+    const uint32_t q = threadIdx.x & 3u;
+    const uint32_t m1 = lane_mask(q & 1u), m2 = lane_mask(q & 2u);
+    return fe_quad_pick(fe_sub(b.Y, b.X), fe_carry(fe_add(b.Y, b.X)), b.T, b.Z, m1, m2);
+}
+
+__device__ __forceinline__ ge_p3 ge_add_quad(const ge_p3& a, const ge_p3& b) {
+    return ge_add_quad_v(a, ge_quad_operand(b));
 }
 
 }  // namespace nw

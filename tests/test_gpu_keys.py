@@ -81,6 +81,19 @@ def test_uncached_strict_golden(bare, golden):
     assert bare.committee_size() == 0
 
 
+@pytest.mark.parametrize("size", [1, 5, 16, 17])
+def test_uncached_strict_golden_small_calls(bare, golden, size):
+    """Calls of at most 16 signatures take the quad-split kernel (k_verify_var<true>: one quad per
+    signature), 17 and more the lane-per-signature kernel: every golden strict verdict in calls of
+    `size` signatures, ragged last call included."""
+    msgs, pks, sigs, want, names = _strict_cases(golden)
+    got = []
+    for f in range(0, len(msgs), size):
+        got += bare.verify_strict_many(msgs[f:f + size], pks[f:f + size], sigs[f:f + size])
+    assert [nm for nm, g, w in zip(names, got, want) if g != w] == []
+    assert any(want) and not all(want)
+
+
 def test_uncached_batch_golden(bare, golden):
     """All 196 golden batches (every adversarial class, cancelling pairs) through the MSM."""
     assert _batch_mismatches(bare, golden) == []
