@@ -199,16 +199,17 @@ __device__ ge_p3 ge_scalarmult_w4_quad(const uint32_t k_in[8], const ge_p3& Q, u
 // One lane per signature (generic messages): P = s B - h A with A decompressed here and h A by
 // ge_scalarmult_w4; writes the same (X, Z, partial flags) record as k_verify, so k_finish completes
 // the strict verdict.  Semantics are those of k_verify with a cached key (nw_core.h).
-// QUAD (at most VAR_QUAD_MAX_SIGS signatures, one 64-thread block): a quad per signature and
-// ge_scalarmult_w4_quad; quads past gn run duplicates (full EXEC) and store nothing.
-static constexpr uint32_t VAR_QUAD_MAX_SIGS = 16;
+// QUAD (at most VAR_QUAD_MAX_SIGS signatures: one-wave blocks of 16 quads, at most one wave per
+// SIMD of the chip): a quad per signature and ge_scalarmult_w4_quad; quads past gn run duplicates
+// (full EXEC) and store nothing.  Above that the lane-per-signature kernel has the throughput.
+static constexpr uint32_t VAR_QUAD_MAX_SIGS = 4096;
 template <bool QUAD>
 __global__ void __launch_bounds__(QUAD ? 64 : 256) k_verify_var(VerifyParams a, uint32_t* scratch) {
-    __shared__ uint32_t qtab[QUAD ? VAR_QUAD_MAX_SIGS * 320 : 1];
+    __shared__ uint32_t qtab[QUAD ? 16 * 320 : 1];
     uint32_t gid;
     bool owner;
     if constexpr (QUAD) {
-        const uint32_t qd = threadIdx.x >> 2;
+        const uint32_t qd = blockIdx.x * 16u + (threadIdx.x >> 2);
         owner = (threadIdx.x & 3u) == 0 && qd < a.gn;
         gid = a.g0 + qd % a.gn;
     } else {
@@ -235,8 +236,10 @@ __global__ void __launch_bounds__(QUAD ? 64 : 256) k_verify_var(VerifyParams a, 
     A = ge_select(A, ge_identity(), !aok);
     const bool asmall = ge_is_identity(ge_dbl(ge_dbl(ge_dbl(A))));
     const uint32_t flags = (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | (asmall ? NW_F_A_SMALL : 0u);
+    // parked by the owner only: a duplicate in another wave (QUAD, more than one block) could
+    // otherwise overwrite the owner's final record (store_prec_soa writes the same row)
     uint32_t* frow = a.pbuf + (size_t)PREC_FLAGS_ROW * a.n;
-    frow[gid] = flags;
+    if (owner) frow[gid] = flags;
     uint32_t s_use[8], zero8[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -624,7 +627,8 @@ hipError_t launch_msm_points_identity(uint32_t npts, const uint32_t* pts, uint8_
 hipError_t launch_verify_var(const VerifyParams& p, int msgmode, uint32_t* scratch, hipStream_t st) {
     if (p.gn == 0) return hipSuccess;
     if (msgmode != 1) return hipErrorInvalidValue;
-    if (p.gn <= VAR_QUAD_MAX_SIGS) hipLaunchKernelGGL(k_verify_var<true>, dim3(1), dim3(64), 0, st, p, scratch);
+    if (p.gn <= VAR_QUAD_MAX_SIGS)
+        hipLaunchKernelGGL(k_verify_var<true>, dim3((p.gn + 15) / 16), dim3(64), 0, st, p, scratch);
     else hipLaunchKernelGGL(k_verify_var<false>, dim3(blocks_for(p.gn, 256)), dim3(256), 0, st, p, scratch);
     return hipGetLastError();
 }

@@ -83,15 +83,33 @@ def test_uncached_strict_golden(bare, golden):
 
 @pytest.mark.parametrize("size", [1, 5, 16, 17])
 def test_uncached_strict_golden_small_calls(bare, golden, size):
-    """Calls of at most 16 signatures take the quad-split kernel (k_verify_var<true>: one quad per
-    signature), 17 and more the lane-per-signature kernel: every golden strict verdict in calls of
-    `size` signatures, ragged last call included."""
+    """Calls of at most 4,096 signatures take the quad-split kernel (k_verify_var<true>: one quad
+    per signature, 16 per one-wave block): every golden strict verdict in calls of `size`
+    signatures (one block, a partial block, two blocks), ragged last call included."""
     msgs, pks, sigs, want, names = _strict_cases(golden)
     got = []
     for f in range(0, len(msgs), size):
         got += bare.verify_strict_many(msgs[f:f + size], pks[f:f + size], sigs[f:f + size])
     assert [nm for nm, g, w in zip(names, got, want) if g != w] == []
     assert any(want) and not all(want)
+
+
+def test_uncached_strict_lane_kernel(bare, golden):
+    """Above 4,096 signatures the lane-per-signature kernel (k_verify_var<false>): the golden strict
+    cases after 4,100 fresh honest signatures, three of them corrupted, in one call."""
+    rng = random.Random(4100)
+    n = 4100
+    seeds = [bytes(rng.randrange(256) for _ in range(32)) for _ in range(n)]
+    hm = [bytes(rng.randrange(256) for _ in range(32)) for _ in range(n)]
+    hp, hs = bare.sign_many(seeds, hm)
+    for i in (0, 2047, 4099):
+        s = bytearray(hs[i])
+        s[i % 32] ^= 0x10
+        hs[i] = bytes(s)
+    msgs, pks, sigs, want, names = _strict_cases(golden)
+    got = bare.verify_strict_many(hm + msgs, hp + pks, hs + sigs)
+    assert got[:n] == [i not in (0, 2047, 4099) for i in range(n)]
+    assert [nm for nm, g, w in zip(names, got[n:], want) if g != w] == []
 
 
 def test_uncached_batch_golden(bare, golden):

@@ -1,5 +1,5 @@
 """Latency of strict verify with keys outside the committee cache (k_verify_var + k_finish), one
-ABI call per sample, at call sizes around the quad / lane kernel switch (16 signatures).
+ABI call per sample, at call sizes around the quad / lane kernel switch (4,096 signatures).
 Usage (GPU box): python tools/strict_latency.py [--samples 200] > gpurun_out/strict_latency.jsonl"""
 import argparse
 import json
@@ -17,7 +17,7 @@ import torch  # noqa: E402,F401  (before libnwcrypto: shared HIP runtime)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--samples", type=int, default=200)
-    ap.add_argument("--sizes", default="1,4,16,17,64")
+    ap.add_argument("--sizes", default="1,16,17,64,256,1024,4096,4097")
     args = ap.parse_args()
     from narwhal_amd import _lib
     eng = _lib.Engine(device=0, key_window=-1)
