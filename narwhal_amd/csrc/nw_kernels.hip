@@ -112,6 +112,9 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
 // chunk), affine x, y, encoding match against R, strict verdict, and (batch mode) compaction of the
 // mismatching signatures into the exact-path list.  Lane L of NL owns the processing-order columns
 // g = L, L + NL, L + 2 NL, ... so every pbuf / pre access of a wave is one contiguous 256-B run.
+// ONE (a.fk == 1, launches up to 65,536 signatures: every latency-bound call): its own kernel, so
+// the chunked path's register allocation is untouched.
+template <bool ONE>
 __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
     const uint32_t NL = (a.gn + a.fk - 1) / a.fk;
     const uint32_t Lr = blockIdx.x * blockDim.x + threadIdx.x;
@@ -124,58 +127,73 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
     const uint32_t cnt = (a.gn - L + NL - 1) / NL;   // columns g0 + L + k NL < g0 + gn  (cnt <= fk)
     const size_t n = a.n;
     const size_t gbase = (size_t)a.g0 + L;
-    // Both chains are fully unrolled over FINISH_K (guarded by cnt) so the column loads are
-    // independent of the running products and issue ahead of them: with one wave per SIMD the
-    // kernel is latency-bound, and a load inside the serial chain would stall it every step.
-    const uint32_t* zrow = a.pbuf + 10 * n;
-    fe acc = fe_one();
-#pragma unroll
-    for (int k = 0; k < FINISH_K; ++k) {
-        if ((uint32_t)k < cnt) {
-            const size_t g = gbase + (size_t)k * NL;
-            acc = fe_mul(acc, load_fe_soa(zrow, n, g));
-            store_fe_soa(a.pre, n, g, acc);   // duplicates store the owner's own values (scratch)
+    // the verdict of column g (flags f): exact-path compaction (batch mode) and the stores
+    auto emit = [&](uint32_t i, uint32_t pf, uint32_t f) {
+        if (a.batch_mode) {
+            if (pf & PF_NOCERT) {
+                f = 0u;   // inside no certificate's range: no message, no verdict, no exact-path entry
+            } else if ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) {
+                // the certificate is rejected (dalek: parse / decode error before the MSM): no
+                // exact-path work for any of its votes
+                atomicOr(&a.cert_state[a.sig_cert[i]], CS_DOOM);
+            } else if (!(f & NW_F_MATCH)) {
+                f |= NW_F_SLOW;
+                const uint32_t t = atomicAdd(a.slow_count, 1u);
+                a.slow_list[t] = i;
+                a.slow_slot[i] = t;
+            }
         }
-    }
-    // Inversion: variable-time safegcd (public data) when each lane chains several signatures
-    // (throughput-bound launches: fewer instructions on average); the branch-free constant-time
-    // divsteps for one signature per lane (latency-bound launches: with 64 independent inversions
-    // per wave the variable-time loop runs the slowest lane's count, measured 10% slower there:
-    // profiles/r02/ab_r02.txt).  a.fk is uniform, so the branch does not diverge.
-    // A launch of a handful of signatures (one header / vote signature) has a handful of active
-    // lanes, so the variable-time loop's cost is that one lane's own count: variable time again.
-    fe inv;
-    if (NW_INV_VAR && (a.fk >= 4 || a.gn <= 8)) inv = fe_invert_var(acc);
-    else inv = fe_invert_sg(acc);
+        a.flags[i] = f;
+        if (a.ok_out) a.ok_out[i] = (f & NW_F_STRICT) ? 1 : 0;
+    };
+    if constexpr (ONE) {
+        // one signature per lane: every load issued before the inversion, no prefix products
+        const fe z = load_fe_soa(a.pbuf + 10 * n, n, gbase);
+        const fe X = load_fe_soa(a.pbuf, n, gbase);
+        const uint32_t pf = a.pbuf[PREC_FLAGS_ROW * n + gbase];
+        const uint32_t i = a.perm ? a.perm[gbase] : (uint32_t)gbase;
+        const fe zi = (NW_INV_VAR && a.gn <= 8) ? fe_invert_var(z) : fe_invert_sg(z);
+        const uint32_t f = finish_x_flags(X, zi, pf);
+        if (owner) emit(i, pf, f);
+        return;
+    } else {
+        // Both chains are fully unrolled over FINISH_K (guarded by cnt) so the column loads are
+        // independent of the running products and issue ahead of them: with one wave per SIMD the
+        // kernel is latency-bound, and a load inside the serial chain would stall it every step.
+        const uint32_t* zrow = a.pbuf + 10 * n;
+        fe acc = fe_one();
 #pragma unroll
-    for (int k = FINISH_K - 1; k >= 0; --k) {
-        if ((uint32_t)k < cnt) {
-            const size_t g = gbase + (size_t)k * NL;
-            fe zi = inv;
-            if (k > 0) {
-                zi = fe_mul(inv, load_fe_soa(a.pre, n, g - NL));
-                inv = fe_mul(inv, load_fe_soa(zrow, n, g));
+        for (int k = 0; k < FINISH_K; ++k) {
+            if ((uint32_t)k < cnt) {
+                const size_t g = gbase + (size_t)k * NL;
+                acc = fe_mul(acc, load_fe_soa(zrow, n, g));
+                store_fe_soa(a.pre, n, g, acc);   // duplicates store the owner's own values (scratch)
             }
-            const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
-            const uint32_t pf = a.pbuf[PREC_FLAGS_ROW * n + g];
-            uint32_t f = finish_x_flags(load_fe_soa(a.pbuf, n, g), zi, pf);
-            if (!owner) continue;
-            if (a.batch_mode) {
-                if (pf & PF_NOCERT) {
-                    f = 0u;   // inside no certificate's range: no message, no verdict, no exact-path entry
-                } else if ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) {
-                    // the certificate is rejected (dalek: parse / decode error before the MSM): no
-                    // exact-path work for any of its votes
-                    atomicOr(&a.cert_state[a.sig_cert[i]], CS_DOOM);
-                } else if (!(f & NW_F_MATCH)) {
-                    f |= NW_F_SLOW;
-                    const uint32_t t = atomicAdd(a.slow_count, 1u);
-                    a.slow_list[t] = i;
-                    a.slow_slot[i] = t;
+        }
+        // Inversion: variable-time safegcd (public data) when each lane chains several signatures
+        // (throughput-bound launches: fewer instructions on average); the branch-free constant-time
+        // divsteps for one signature per lane (latency-bound launches: with 64 independent inversions
+        // per wave the variable-time loop runs the slowest lane's count, measured 10% slower there:
+        // profiles/r02/ab_r02.txt).  a.fk is uniform, so the branch does not diverge.
+        // A launch of a handful of signatures (one header / vote signature) has a handful of active
+        // lanes, so the variable-time loop's cost is that one lane's own count: variable time again.
+        fe inv;
+        if (NW_INV_VAR && (a.fk >= 4 || a.gn <= 8)) inv = fe_invert_var(acc);
+        else inv = fe_invert_sg(acc);
+#pragma unroll
+        for (int k = FINISH_K - 1; k >= 0; --k) {
+            if ((uint32_t)k < cnt) {
+                const size_t g = gbase + (size_t)k * NL;
+                fe zi = inv;
+                if (k > 0) {
+                    zi = fe_mul(inv, load_fe_soa(a.pre, n, g - NL));
+                    inv = fe_mul(inv, load_fe_soa(zrow, n, g));
                 }
+                const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
+                const uint32_t pf = a.pbuf[PREC_FLAGS_ROW * n + g];
+                const uint32_t f = finish_x_flags(load_fe_soa(a.pbuf, n, g), zi, pf);
+                if (owner) emit(i, pf, f);
             }
-            a.flags[i] = f;
-            if (a.ok_out) a.ok_out[i] = (f & NW_F_STRICT) ? 1 : 0;
         }
     }
 }
@@ -474,7 +492,8 @@ hipError_t launch_finish(const VerifyParams& p, hipStream_t st) {
     if (p.gn == 0) return hipSuccess;
     if (p.fk < 1 || p.fk > (uint32_t)FINISH_K || (uint64_t)p.g0 + p.gn > p.n) return hipErrorInvalidValue;
     const uint64_t lanes = (p.gn + p.fk - 1) / p.fk;
-    hipLaunchKernelGGL(k_finish, dim3(blocks_for(lanes, 256)), dim3(256), 0, st, p);
+    if (p.fk == 1) hipLaunchKernelGGL(k_finish<true>, dim3(blocks_for(lanes, 256)), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(k_finish<false>, dim3(blocks_for(lanes, 256)), dim3(256), 0, st, p);
     return hipGetLastError();
 }
 
