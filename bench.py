@@ -86,7 +86,7 @@ def traffic_per_launch():
 
 def clock_frac_profile():
     """k_verify's fraction of the MAD peak per shader cycle (both kernels timed in cycles by PMC
-    GRBM_GUI_ACTIVE: tools/r04_pmc.sh + tools/clock_frac.py -> profiles/r04/clock_frac_r04h.json)."""
+    GRBM_GUI_ACTIVE: a gpu_pmc.sh pass + tools/clock_frac.py -> profiles/r04/clock_frac_r04h.json)."""
     path = os.path.join(ROOT, "profiles", "r04", "clock_frac_r04h.json")
     if not os.path.exists(path):
         return None
@@ -111,6 +111,27 @@ def cgroup_cpu_quota():
         return None if q == "max" else float(q) / float(per)
     except (OSError, ValueError):
         return None
+
+
+def host_topology():
+    """(physical cores, logical CPUs) of the whole host, from sysfs topology (a container sees the
+    host's CPUs there even when its cgroup quota is far smaller)."""
+    import glob
+    cores, logical = set(), 0
+    for d in glob.glob("/sys/devices/system/cpu/cpu[0-9]*/topology"):
+        try:
+            with open(os.path.join(d, "physical_package_id")) as f:
+                pkg = f.read().strip()
+            with open(os.path.join(d, "core_id")) as f:
+                core = f.read().strip()
+        except OSError:
+            continue
+        cores.add((pkg, core))
+        logical += 1
+    if not cores:
+        n = os.cpu_count() or 1
+        return n, n
+    return len(cores), logical
 
 
 def cpu_model():
@@ -169,9 +190,25 @@ def cpu_baseline(cs, com, seconds, probe_seconds=2.5, label="C2"):
     else:
         threads = cands[0]
     rate, done_sigs, done_certs, dt = run(threads, seconds)
+    # The measured slice is the container's CPU quota, not the host.  Per quota CPU (one CPU-second
+    # per second of wall time) the rate extrapolates to the host's physical cores (conservative: an
+    # SMT sibling is counted as no extra capacity) and, as an upper bound, to its logical CPUs.
+    quota = cgroup_cpu_quota()
+    slice_cpus = quota if quota else float(threads)
+    per_cpu = rate / slice_cpus
+    phys, logical = host_topology()
+    host_rate = per_cpu * phys
     return {"value": rate, "unit": "sigs/s", "cores": threads, "kind": "port",
-            "per_gpu_share": {"value": rate / GPUS_PER_NODE, "cores": threads / GPUS_PER_NODE,
-                              "note": "host rate / %d GPUs per node" % GPUS_PER_NODE},
+            "measured_slice": {"cpus": slice_cpus, "threads": threads,
+                               "note": "cgroup CPU quota of this process (the value above is measured on it)"},
+            "per_cpu": {"value": per_cpu, "unit": "sigs/s per quota CPU"},
+            "host_extrapolated": {"value": host_rate, "physical_cores": phys, "logical_cpus": logical,
+                                  "upper_bound_logical": per_cpu * logical,
+                                  "note": "EXTRAPOLATED, not measured: per_cpu x the host's physical cores "
+                                          "(SMT siblings counted as no extra capacity); upper_bound_logical = "
+                                          "per_cpu x logical CPUs"},
+            "per_gpu_share": {"value": host_rate / GPUS_PER_NODE, "cores": phys / GPUS_PER_NODE,
+                              "note": "host_extrapolated / %d GPUs per node" % GPUS_PER_NODE},
             "cpu_model": cpu_model(),
             # the affinity mask can be far wider than the cgroup's CPU quota (GPU box: 256 vs 16);
             # threads beyond ~2x the quota only time-slice (profiles/r02/cpu_probe_r02.json)
@@ -907,7 +944,12 @@ def main(argv=None):
             cb = cpu_baseline(cs, com, args.cpu_seconds, label=args.config)
             if ndig:
                 cb["with_digests"] = cpu_step_with_digests(cb, host_b, plan, args.cpu_seconds / 3)
-            cb["gpu_over_cpu"] = value / cb["value"]
+            cb["gpu_over_cpu"] = value / cb["value"]          # against the measured slice
+            cb["gpu_over_host_extrapolated"] = value / cb["host_extrapolated"]["value"]   # against the whole host
+            cb["ratios_note"] = ("gpu_over_cpu: this run's %d GPU(s) vs the measured %.0f-CPU slice; "
+                                 "gpu_over_host_extrapolated: vs the whole host's %d physical cores (north star: "
+                                 ">= 50x the host at 8 GPUs)" % (world, cb["measured_slice"]["cpus"],
+                                                                  cb["host_extrapolated"]["physical_cores"]))
             if ndig:
                 cb["with_digests"]["gpu_over_cpu"] = value / cb["with_digests"]["sigs_per_s"]
             out["cpu_baseline"] = cb

@@ -70,16 +70,24 @@ typedef struct nw_ctx nw_ctx;
 typedef struct nw_opts {
     int device;        /* HIP device ordinal (one process per GPU; -1 = current device) */
     uint32_t flags;    /* reserved, 0 */
-    size_t max_keys;   /* key-cache capacity in keys (0 = fill a 160 GiB HBM budget) */
+    size_t max_keys;   /* key-cache capacity in keys.  0 = as many as the key budget holds.  The key
+                          budget is the HBM free on the device at the first nw_committee_load (after
+                          this context's basepoint table and anything other contexts or processes
+                          hold) less a workspace reserve of max(16 GiB, 1/16 of HBM): ~258 GB on an
+                          otherwise idle MI355X.  In committee mode (key_window -1) a non-zero
+                          max_keys declares every key the context will ever load: the window is sized
+                          for max_keys keys and the first load allocates all of them at once (the
+                          worker's two Processors: max_keys = 200,000, two loads of 100,000). */
     int key_window;    /* key comb window: 8, 9, 12, 13, 16 or 20 bits.  0 = auto at the first load (16
                           for <= 384 keys, 12 for <= 12288 keys, else 8); -1 = committee mode: the
-                          first nw_committee_load is the committee, and the widest window whose
-                          tables fit the key budget with 25% headroom is used (W20 up to 157 keys,
-                          W16 up to 2,047, W13 up to 13,104: a 10,000-validator committee; W12 up to 23,819;
-                          W9 up to 144,068: the worker's 100,000 keys).  Table
-                          bytes per key: w8 0.53 MB, w9 0.95 MB, w12 5.77 MB, w13 10.5 MB,
-                          w16 67.1 MB, w20 872 MB; additions per signature 32 / 29 / 22 / 20 / 16 / 13.  (The
-                          basepoint comb is fixed at w24: 11 additions, 11.8 GB per context.) */
+                          widest window whose tables fit the key budget is used, for max_keys keys
+                          when set, else for the first load's keys with 25% headroom (on an idle
+                          MI355X: W20 up to ~236 keys, W16 up to ~3,000, W13 up to ~19,600: a
+                          10,000-validator committee; W9 up to ~216,000: the worker's 100,000 keys,
+                          or its 200,000 declared through max_keys).  Table bytes per key: w8 0.53 MB,
+                          w9 0.95 MB, w12 5.77 MB, w13 10.5 MB, w16 67.1 MB, w20 872 MB; additions per
+                          signature 32 / 29 / 22 / 20 / 16 / 13.  (The basepoint comb is fixed at w24:
+                          11 additions, 11.8 GB per context.) */
 } nw_opts;
 
 /* One certificate: its votes are sig[first_vote .. first_vote + n_votes). */
@@ -216,7 +224,10 @@ int nw_sha512_many_dev(nw_ctx* ctx, const uint8_t* d_base, const uint64_t* d_off
  * digest kernel and the download and returns a job at once.
  *   nw_job_done(job): 1 when the digests are ready, 0 while in flight, < 0 on a device error.
  *   nw_job_wait(job): blocks until out (n x 64 bytes) holds the digests, then frees the job; every
- *                     job must be waited for exactly once, before nw_ctx_destroy. */
+ *                     job must be waited for exactly once, before nw_ctx_destroy.
+ * A job holds one of the context's 64 call workspaces until it is waited for; at most 32 jobs may be
+ * unwaited at once (the rest of the pool stays for synchronous calls): a 33rd submit returns
+ * NW_ERR_NOMEM at once rather than blocking. */
 typedef struct nw_job nw_job;
 int nw_sha512_many_async(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, size_t n,
                          uint8_t (*out)[64], nw_job** job);

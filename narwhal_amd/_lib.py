@@ -494,7 +494,7 @@ class DigestJob:
     def __init__(self, engine: Engine, messages):
         import numpy as np
         self._engine = engine
-        self._msgs = [m if isinstance(m, np.ndarray) else np.frombuffer(m, np.uint8) for m in messages]
+        self._msgs = [self._as_bytes(m) for m in messages]
         n = len(self._msgs)
         self.n = n
         self._ptrs = np.array([m.ctypes.data if m.size else 0 for m in self._msgs], np.uint64)
@@ -503,6 +503,17 @@ class DigestJob:
         self._job = ctypes.c_void_p()
         engine.check(LIB.nw_sha512_many_async(engine.handle, self._ptrs.ctypes.data, self._lens.ctypes.data, n,
                                               self._out.ctypes.data, ctypes.byref(self._job)), "nw_sha512_many_async")
+
+    @staticmethod
+    def _as_bytes(m):
+        """A flat uint8 view of one message: the pointer and byte length the ABI gets must describe
+        its bytes.  Non-uint8 or non-contiguous arrays raise rather than hash the wrong bytes."""
+        import numpy as np
+        if isinstance(m, np.ndarray):
+            if m.dtype != np.uint8 or not m.flags.c_contiguous:
+                raise TypeError("DigestJob: messages must be bytes-like or C-contiguous uint8 arrays")
+            return m.reshape(-1)
+        return np.frombuffer(m, np.uint8)
 
     def done(self) -> bool:
         if not self._job:

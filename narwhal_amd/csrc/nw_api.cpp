@@ -157,6 +157,10 @@ struct Workspace {
 };
 
 constexpr size_t kMaxWorkspaces = 64;   // one per concurrently calling thread (the worker's 64)
+// Asynchronous digest jobs hold a workspace from submit to nw_job_wait; past this many unwaited jobs
+// a submit fails at once (NW_ERR_NOMEM) instead of blocking on a pool that only those jobs' own
+// waits could refill.  The other half of the pool stays for synchronous calls.
+constexpr int kMaxAsyncJobs = (int)kMaxWorkspaces / 2;
 
 }  // namespace
 
@@ -170,6 +174,9 @@ struct nw_ctx {
     size_t max_keys = 0;          // 0: derived from the HBM budget once the window is fixed
     bool max_keys_user = false;
     int key_window = 0;           // 0: not yet decided (first load)
+    bool committee_mode = false;  // nw_opts.key_window == -1
+    bool key_reserve = false;     // committee mode + max_keys: the first load allocates max_keys slots
+    bool budget_fixed = false;    // window, max_keys and reservation decided (first load with keys)
     size_t key_words = 0;         // u32 words per key table
     size_t nkeys = 0, key_cap = 0;
     uint32_t* d_keys_raw = nullptr;
@@ -184,6 +191,7 @@ struct nw_ctx {
     std::condition_variable pool_cv;
     std::vector<std::unique_ptr<Workspace>> pool;
     std::vector<Workspace*> free_ws;
+    std::atomic<int> async_jobs{0};   // unwaited nw_sha512_many_async jobs (<= kMaxAsyncJobs)
     // measurement: (start, stop) event pairs around k_verify launches
     std::mutex prof_mu;
     bool prof_on = false;
@@ -265,11 +273,10 @@ public:
     }
     ~Lease() {
         if (!ws_) return;
-        if (sync_on_release_ && stream_) {
-            (void)hipStreamSynchronize(stream_);
-            ws_->pending = false;
-        }
+        const bool drain = sync_on_release_ && stream_;
+        if (drain) (void)hipStreamSynchronize(stream_);
         std::lock_guard<std::mutex> g(ctx_->pool_mu);
+        if (drain) ws_->pending = false;
         ctx_->free_ws.push_back(ws_);
         ctx_->pool_cv.notify_one();
     }
@@ -283,6 +290,7 @@ public:
     hipError_t finish() {
         hipError_t e = hipEventRecord(ws_->done, stream_);
         if (e == hipSuccess) {
+            std::lock_guard<std::mutex> g(ctx_->pool_mu);
             ws_->pending = true;
             ws_->last = stream_;
         }
@@ -290,6 +298,7 @@ public:
     }
     // a host-buffer call that completed: its stream is idle
     void synced() {
+        std::lock_guard<std::mutex> g(ctx_->pool_mu);   // drain_all reads pending under pool_mu
         ws_->pending = false;
         sync_on_release_ = false;
     }
@@ -310,13 +319,20 @@ struct nw_job {
     uint8_t* out = nullptr;
     size_t n = 0;
     size_t o_out = 0;
+    std::atomic<int>* inflight = nullptr;   // the context's async job count (released with the job)
+    ~nw_job() {
+        lease.reset();
+        if (inflight) inflight->fetch_sub(1);
+    }
 };
 
 namespace {
 
-// Wait for every call that may still read the key tables (exclusive key lock held).  Every lease
-// is taken under the shared key lock, so no lease is live here and nothing else touches
-// pending/done while we read them.
+// Wait for every call that may still read the key tables (exclusive key lock held).  Every
+// verification lease is taken under the shared key lock, so none is live here.  Asynchronous
+// digest jobs (nw_sha512_many_async) hold their lease WITHOUT the key lock, so one may be live: it
+// reads no key table, its completion event is only re-recorded by its own submit, and every write
+// of ``pending`` (Lease::finish / synced / release) happens under pool_mu, as these reads do.
 int drain_all(nw_ctx* ctx) {
     std::lock_guard<std::mutex> g(ctx->pool_mu);
     for (auto& w : ctx->pool)
@@ -353,7 +369,18 @@ static_assert(NW_FK_FIXED >= 0 && NW_FK_FIXED <= FINISH_K, "NW_FK_FIXED: 0 (adap
 // no chain; C2's million signatures get 16 per lane.
 uint32_t finish_k_for(const nw_ctx* ctx, size_t n);
 
-constexpr size_t KEY_CACHE_BUDGET = 160ull << 30;  // bytes of HBM for key tables by default (of 288 GB)
+// HBM for key tables: what the device has free at the first committee load (after this context's
+// basepoint table and whatever other contexts or processes on the GPU hold), less a reserve for call
+// workspaces.  A node may run its primary and a worker on one GPU; a fixed share per context could
+// not see the other.
+constexpr size_t kWorkspaceReserve = 16ull << 30;   // at least this much stays free for workspaces
+size_t key_budget(nw_ctx* ctx) {
+    size_t free_b = 0, total_b = 0;
+    if (hipSetDevice(ctx->device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess || total_b == 0)
+        return 0;
+    const size_t reserve = std::max(kWorkspaceReserve, total_b / 16);
+    return free_b > reserve ? free_b - reserve : 0;
+}
 // Group signatures by signer (key-table locality) above this batch size, and only when keys repeat
 // (at least kGroupMinSigsPerKey signatures per cached key on average): the worker's load (62,500
 // signatures over 100,000 keys, each key at most once) gains nothing from the order and would pay
@@ -362,34 +389,43 @@ constexpr size_t kGroupMinSigs = 16384;
 constexpr size_t kGroupMinSigsPerKey = 4;
 
 // Key comb window, fixed at the first load.  Auto (0): a conservative choice that leaves room for
-// keys added later.  Committee mode (-1): the first load IS the committee; take the widest window
-// whose tables for it fit the key budget with 25% headroom (fewest additions per signature).
-int committee_window(size_t n, size_t budget) {
+// keys added later.  Committee mode (-1): take the widest window (fewest additions per signature)
+// whose tables fit the budget for ``n`` keys times ``headroom``:
+//   - without nw_opts.max_keys the first load IS the committee, with 25% headroom for later keys;
+//   - with nw_opts.max_keys the caller has declared every key it will load (the worker's two
+//     Processors, 2 x 100,000 simulation keys, worker/src/processor.rs:46-58 and worker.rs:182,228):
+//     sized for exactly that many, and the cache is allocated for all of them at the first load
+//     (grow_keys), so the second Processor's load appends without a growth copy.
+int committee_window(size_t n, double headroom, size_t budget) {
     for (int w : {20, 16, 13, 12, 9}) {
-        const double need = 1.25 * (double)n * (double)comb_words(w) * 4.0;
+        const double need = headroom * (double)n * (double)comb_words(w) * 4.0;
         if (need <= (double)budget) return w;
     }
     return 8;
 }
 
 void fix_window(nw_ctx* ctx, size_t first_load) {
-    const size_t budget = ctx->max_keys_user ? (size_t)-1 : KEY_CACHE_BUDGET;
-    if (ctx->key_window == -1) ctx->key_window = committee_window(first_load, budget);
+    const size_t budget = key_budget(ctx);
+    if (ctx->key_window == -1)
+        ctx->key_window = ctx->max_keys_user ? committee_window(std::max(ctx->max_keys, first_load), 1.0, budget)
+                                             : committee_window(first_load, 1.25, budget);
     if (ctx->key_window == 0) ctx->key_window = first_load <= 384 ? 16 : (first_load <= 12288 ? 12 : 8);
     ctx->key_words = comb_words(ctx->key_window);
-    if (!ctx->max_keys_user) ctx->max_keys = KEY_CACHE_BUDGET / (ctx->key_words * 4);
+    ctx->key_reserve = ctx->max_keys_user && ctx->committee_mode;
+    ctx->budget_fixed = true;
+    if (!ctx->max_keys_user) ctx->max_keys = budget / (ctx->key_words * 4);
 }
 
 int grow_keys(nw_ctx* ctx, size_t need) {
     if (need <= ctx->key_cap) return NW_OK;
     if (need > ctx->max_keys) {
-        set_error(ctx, "key cache capacity exceeded (nw_opts.max_keys)");
+        set_error(ctx, "key cache capacity exceeded (nw_opts.max_keys, or the HBM free at the first load)");
         return NW_ERR_NOMEM;
     }
     // The first load sizes the cache to its keys (rounded up to 64): in committee mode it IS the
     // committee, and doubling from 64 would reserve up to 2x the tables (16,384 W13 tables = 172 GB
     // for a 10,000-key committee, against 105 GB used).  Later loads grow it by doubling.
-    size_t cap = ctx->key_cap ? ctx->key_cap : (need + 63) / 64 * 64;
+    size_t cap = ctx->key_cap ? ctx->key_cap : (ctx->key_reserve ? ctx->max_keys : (need + 63) / 64 * 64);
     while (cap < need) cap *= 2;
     if (cap > ctx->max_keys) cap = ctx->max_keys;
     uint32_t *raw = nullptr, *info = nullptr, *stake = nullptr, *tab = nullptr;
@@ -484,7 +520,7 @@ int ensure_slots(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, si
     if (add == 0 && refresh.empty()) return NW_OK;
     int rc = drain_all(ctx);   // nothing in flight may read the tables or the stakes we change
     if (rc != NW_OK) return rc;
-    if (add && ctx->key_window <= 0) fix_window(ctx, add);
+    if (add && !ctx->budget_fixed) fix_window(ctx, add);
     if (add) {
         rc = grow_keys(ctx, ctx->nkeys + add);
         if (rc != NW_OK) return rc;
@@ -1158,7 +1194,8 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     }
     if (opts && opts->key_window) {
         ctx->key_window = opts->key_window;
-        if (ctx->key_window > 0) fix_window(ctx, 0);
+        ctx->committee_mode = ctx->key_window == -1;
+        if (ctx->key_window > 0) ctx->key_words = comb_words(ctx->key_window);   // budget: at the first load
     }
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
@@ -1638,6 +1675,12 @@ int nw_sha512_many_async(nw_ctx* ctx, const uint8_t* const* msg, const size_t* l
         return NW_OK;
     }
     NW_TRY(hipSetDevice(ctx->device), "hipSetDevice");
+    if (ctx->async_jobs.fetch_add(1) >= kMaxAsyncJobs) {
+        ctx->async_jobs.fetch_sub(1);
+        set_error(ctx, "nw_sha512_many_async: too many unwaited jobs (limit 32; wait for one first)");
+        return NW_ERR_NOMEM;
+    }
+    j->inflight = &ctx->async_jobs;
     std::vector<uint64_t> off(n);
     size_t total = 0;
     for (size_t i = 0; i < n; ++i) {

@@ -112,8 +112,9 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
 // chunk), affine x, y, encoding match against R, strict verdict, and (batch mode) compaction of the
 // mismatching signatures into the exact-path list.  Lane L of NL owns the processing-order columns
 // g = L, L + NL, L + 2 NL, ... so every pbuf / pre access of a wave is one contiguous 256-B run.
-// ONE (a.fk == 1, launches up to 65,536 signatures: every latency-bound call): its own kernel, so
-// the chunked path's register allocation is untouched.
+// ONE (a.fk == 1: finish_k_for gives it to launches of up to 256 x 4 x 64 = 262,144 signatures,
+// i.e. every latency-bound call and mid-size batches up to one lane per SIMD slot): its own kernel,
+// so the chunked path's register allocation is untouched.
 template <bool ONE>
 __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
     const uint32_t NL = (a.gn + a.fk - 1) / a.fk;
@@ -220,15 +221,20 @@ __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
     // certificate; only the in-range votes are read
     const bool range_bad = (uint64_t)first + a.cert_n[c] > a.nsigs;
     const uint32_t nv = range_bad ? (first < a.nsigs ? a.nsigs - first : 0u) : a.cert_n[c];
-    bool bad = range_bad, slow = false;
+    // CS_DOOM: a bad S / undecodable A (the flags say so too) or a vote range overlapping another
+    // certificate's (k_expand_count)
+    bool bad = range_bad || (a.cert_state && (a.cert_state[c] & CS_DOOM)), slow = false;
     uint32_t tsum = 0;
     uint64_t stake = 0;
     for (uint32_t v = lane; v < nv; v += 64) {
         const uint32_t f = a.flags[first + v];
-        bad = bad || ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) || (f & NW_F_R_BAD);
+        // a vote this certificate does not own (overlapping device ranges, NW_ERR_ARG) was checked
+        // against its owner's message: it rejects this certificate and adds none of its stake
+        const bool own = a.sig_cert[first + v] == c;
+        bad = bad || !own || ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) || (f & NW_F_R_BAD);
         slow = slow || (f & NW_F_SLOW);
         tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
-        if (f & NW_F_STRICT) stake += a.stake[a.signer[first + v]];
+        if (own && (f & NW_F_STRICT)) stake += a.stake[a.signer[first + v]];
     }
     bad = __any(bad);
     slow = __any(slow);
@@ -343,7 +349,7 @@ static constexpr uint32_t EXPAND_CERTS_PER_BLOCK = 4;   // one wave each
 __global__ void __launch_bounds__(256) k_expand_count(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys,
                                                       const uint32_t* cert_first, const uint32_t* cert_n,
                                                       const uint32_t* signer, uint32_t* sig_cert, uint32_t* counts,
-                                                      uint32_t* status) {
+                                                      uint32_t* status, uint32_t* cert_state) {
     extern __shared__ uint32_t hist[];
     // one wave per certificate: its lanes write the vote -> certificate entries side by side (a
     // thread per certificate would store 667 / 6,667 entries serially at C3 / C4)
@@ -353,7 +359,18 @@ __global__ void __launch_bounds__(256) k_expand_count(uint32_t ncerts, uint32_t 
         const uint32_t f = cert_first[c], n = cert_n[c];
         bad = lane == 0 && (uint64_t)f + n > nsigs;
         const uint32_t end = (uint64_t)f + n > nsigs ? nsigs : f + n;   // clamped: k_cert_finalize rejects it
-        for (uint32_t v = f + lane; v < end; v += 64) bad = (atomicExch(&sig_cert[v], c) != NO_CERT) || bad;
+        for (uint32_t v = f + lane; v < end; v += 64) {
+            const uint32_t prev = atomicExch(&sig_cert[v], c);
+            if (prev != NO_CERT) {
+                // a vote claimed twice: whichever certificate the map ends with checks it against its
+                // own message, so BOTH are doomed (k_cert_finalize rejects them), in any order
+                bad = true;
+                if (cert_state) {
+                    atomicOr(&cert_state[c], CS_DOOM);
+                    if (prev < ncerts) atomicOr(&cert_state[prev], CS_DOOM);
+                }
+            }
+        }
     }
     const uint32_t t0 = blockIdx.x * GROUP_TILE;
     if ((counts || status) && t0 < nsigs) {
@@ -518,7 +535,7 @@ hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, c
     if (nb == 0) return hipGetLastError();
     const size_t lds = counts && nkeys <= GROUP_LDS_KEYS ? (size_t)nkeys * 4 : 0;
     hipLaunchKernelGGL(k_expand_count, dim3(nb), dim3(256), lds, st, ncerts, nsigs, nkeys, first, nv, signer, sig_cert,
-                       counts, status);
+                       counts, status, cert_state);
     return hipGetLastError();
 }
 

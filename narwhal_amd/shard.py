@@ -94,17 +94,37 @@ def allgather_digests(digests_local, group=None):
     return out
 
 
-def verify_sharded(engine, cs, slots, zseed: bytes, rank: int, world: int, group=None, device=None):
-    """Verify this rank's shard of ``cs`` (narwhal_amd.workload.Certificates) on its GPU and
-    all-gather the node-wide verdicts.  Returns (cert_ok uint8[C], stake int64[C]) torch tensors on
-    ``device`` (default: this rank's GPU)."""
-    import torch
+def shard_inputs(cs, slots, rank: int, world: int, cert_base: int = 0):
+    """This rank's share of ``cs`` (narwhal_amd.workload.Certificates with contiguous vote ranges):
+    a dict with ``ranges`` (every rank's [c0, c1)), ``cert_base`` = cert_base + c0 (the GLOBAL index of
+    its first certificate: the NW-Z coefficient nonce, so the shard's verdicts equal the one-GPU
+    verdicts of a call with batch index ``cert_base``),
+    and its rebased arrays ``first``, ``n``, ``sigs``, ``signer_slots``, ``msgs``."""
     ranges = partition(cs.cert_n, world)
     c0, c1 = ranges[rank]
     f0 = int(cs.cert_first[c0]) if c1 > c0 else 0
     f1 = int(cs.cert_first[c1 - 1] + cs.cert_n[c1 - 1]) if c1 > c0 else 0
-    ok, _, st = engine.verify_certs_np(cs.cert_first[c0:c1] - f0, cs.cert_n[c0:c1], cs.sigs[f0:f1],
-                                       slots[cs.signer[f0:f1]], cs.msgs[c0:c1], zseed, cert_base=c0)
+    return {"ranges": ranges, "cert_base": cert_base + c0,
+            "first": np.ascontiguousarray(cs.cert_first[c0:c1] - f0, dtype=np.uint32),
+            "n": np.ascontiguousarray(cs.cert_n[c0:c1], dtype=np.uint32),
+            "sigs": cs.sigs[f0:f1], "signer_slots": np.asarray(slots)[cs.signer[f0:f1]], "msgs": cs.msgs[c0:c1]}
+
+
+def verify_shard(engine, cs, slots, zseed: bytes, rank: int, world: int, cert_base: int = 0):
+    """The GPU half of one rank's step: (ranges, cert_ok u8[c1-c0], accepted_stake u64[c1-c0])."""
+    sh = shard_inputs(cs, slots, rank, world, cert_base)
+    ok, _, st = engine.verify_certs_np(sh["first"], sh["n"], sh["sigs"], sh["signer_slots"], sh["msgs"], zseed,
+                                       cert_base=sh["cert_base"])
+    return sh["ranges"], ok, st
+
+
+def verify_sharded(engine, cs, slots, zseed: bytes, rank: int, world: int, group=None, device=None,
+                   cert_base: int = 0):
+    """Verify this rank's shard of ``cs`` (narwhal_amd.workload.Certificates) on its GPU and
+    all-gather the node-wide verdicts.  Returns (cert_ok uint8[C], stake int64[C]) torch tensors on
+    ``device`` (default: this rank's GPU)."""
+    import torch
+    ranges, ok, st = verify_shard(engine, cs, slots, zseed, rank, world, cert_base)
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
     return allgather_verdicts(torch.from_numpy(ok).to(dev), torch.from_numpy(st.astype(np.int64)).to(dev), ranges,
                               group)
@@ -125,17 +145,30 @@ def verify_split_batch(engine, msgs, pks, sigs, zseed: bytes, batch_index: int, 
     exact, so the verdict equals the unsplit nw_verify_batch verdict."""
     import torch
     import torch.distributed as dist
+    row = split_partial_row(engine, msgs, pks, sigs, zseed, batch_index, rank, world)
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    buf = torch.from_numpy(row).to(dev)
+    gathered = [torch.empty_like(buf) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(gathered, buf, group=group)
+    return split_verdict(engine, [g.cpu().numpy() for g in gathered])
+
+
+def split_partial_row(engine, msgs, pks, sigs, zseed: bytes, batch_index: int, rank: int, world: int):
+    """This rank's all-gather row for ``verify_split_batch``: uint8[POINT_BYTES + 8] = its partial
+    point, then its parse/decode failure flag."""
     from ._lib import POINT_BYTES
     a, b = split_bounds(len(sigs), world)[rank]
     pt, bad = engine.verify_batch_partial(msgs[a:b], pks[a:b], sigs[a:b], zseed, batch_index, a)
-    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
-    buf = torch.zeros(POINT_BYTES + 8, dtype=torch.uint8)
-    buf[:POINT_BYTES] = torch.frombuffer(bytearray(pt), dtype=torch.uint8)
-    buf[POINT_BYTES] = 1 if bad else 0
-    buf = buf.to(dev)
-    gathered = [torch.empty_like(buf) for _ in range(dist.get_world_size(group))]
-    dist.all_gather(gathered, buf, group=group)
-    rows = [g.cpu().numpy() for g in gathered]
+    row = np.zeros(POINT_BYTES + 8, np.uint8)
+    row[:POINT_BYTES] = np.frombuffer(bytes(pt), np.uint8)
+    row[POINT_BYTES] = 1 if bad else 0
+    return row
+
+
+def split_verdict(engine, rows) -> bool:
+    """The batch verdict from every rank's row (in rank order): Err if any shard failed to parse or
+    decode, else Ok iff the partial points sum to the identity."""
+    from ._lib import POINT_BYTES
     if any(int(r[POINT_BYTES]) for r in rows):
         return False
     return engine.points_sum_is_identity([bytes(r[:POINT_BYTES]) for r in rows])

@@ -19,19 +19,130 @@ per-chain rate.  So the drop-in for :65 is not one ``nw_sha512`` per batch but o
   window is delivered only after every earlier window, exactly like the serial loop's order.
 
 ``Processor`` mirrors the reference object on top of it: store + the serialized
-``WorkerPrimaryMessage`` in arrival order.  The simulated verify load (:67-81) is the separate
-``nw_verify_batches`` / ``nw_verify_batches_pk`` path.  Host logic only: every
-digest comes from libnwcrypto; there is no CPU hashing in this module.
+``WorkerPrimaryMessage`` in arrival order, and, when given a ``VerifyLoad``, the simulated signature
+verification of :67-81 on every batch.
+
+The simulated load (``VerifyLoad``).  Each of a worker's TWO Processors (own batches,
+worker/src/worker.rs:182; other workers' batches, :228) makes 100,000 fresh keypairs at spawn and
+signs the 8-byte LE messages 0..99,999 (processor.rs:46-58); per batch it verifies the first
+``min(100,000, #tx)`` of them as 64 ``verify_batch`` chunks and unwraps every verdict (:67-81).
+A worker process therefore holds 200,000 distinct keys.  The drop-in: the worker's engine is
+created in committee mode with the two Processors' keys declared up front (``worker_engine``:
+``max_keys`` = 200,000), so the first Processor's load sizes the comb window for all of them (W9 on
+an idle MI355X: 190 GB of tables) and the second appends without a growth copy.  The worker loads
+no committee (it verifies no committee signature).  Each batch's 64 chunks are ONE
+``nw_verify_batches`` call on the cached comb tables.  Host logic only: every digest and verdict
+comes from libnwcrypto; there is no CPU hashing or verification in this module.
 """
 from __future__ import annotations
 
+import os
 import struct
+import warnings
 from collections import deque
 from typing import Deque, Iterable, Iterator, List, MutableMapping, Optional, Tuple
 
 from . import _lib
 
 OUR_BATCH, OTHERS_BATCH = 0, 1   # WorkerPrimaryMessage variant indices (primary/src/primary.rs:51-56)
+SIM_KEYS = 100_000                # simulated-load keypairs per Processor (worker/src/processor.rs:47)
+PROCESSORS_PER_WORKER = 2         # own batches (worker/src/worker.rs:182) + others' batches (:228)
+SIM_CHUNKS = 64                   # verify_batch chunks per batch (processor.rs:75)
+WORKER_MSG_BATCH = 0              # WorkerMessage::Batch variant index (worker/src/worker.rs:37-40)
+
+
+class VerificationPanic(RuntimeError):
+    """The reference ``.unwrap()``s every chunk verdict (processor.rs:78): a failing chunk panics
+    the Processor task."""
+
+
+def worker_engine(device: int = -1, processors: int = PROCESSORS_PER_WORKER, keys: int = SIM_KEYS):
+    """The worker process's engine: committee mode (key_window -1) with every
+    simulated-load key declared through ``max_keys``, so both Processors' loads are cached on one
+    comb window and one allocation."""
+    return _lib.Engine(device=device, max_keys=processors * keys, key_window=-1)
+
+
+def batch_tx_count(batch) -> int:
+    """Transactions in a serialized ``WorkerMessage`` (bincode 1.3: u32 LE variant; ``Batch`` =
+    u64 LE count, then each transaction as u64 LE length + bytes).  Returns -1 for another variant
+    (``BatchRequest``: the reference's ``if let WorkerMessage::Batch`` does not verify it).  A
+    malformed message raises ValueError where the reference's ``deserialize(..).unwrap()`` panics
+    (processor.rs:68)."""
+    mv = memoryview(batch).cast("B")
+    if len(mv) < 4:
+        raise ValueError("WorkerMessage: truncated variant")
+    (variant,) = struct.unpack_from("<I", mv, 0)
+    if variant != WORKER_MSG_BATCH:
+        if variant == 1:
+            return -1
+        raise ValueError("WorkerMessage: unknown variant %d" % variant)
+    if len(mv) < 12:
+        raise ValueError("WorkerMessage::Batch: truncated length")
+    (n,) = struct.unpack_from("<Q", mv, 4)
+    pos = 12
+    for _ in range(n):
+        if pos + 8 > len(mv):
+            raise ValueError("WorkerMessage::Batch: truncated transaction")
+        (ln,) = struct.unpack_from("<Q", mv, pos)
+        pos += 8 + ln
+        if pos > len(mv):
+            raise ValueError("WorkerMessage::Batch: truncated transaction")
+    return n
+
+
+def sim_chunks(count: int):
+    """processor.rs:76-77: chunk c covers [count*c/64, min(count, count*(c+1)/64))."""
+    import numpy as np
+    c = np.arange(SIM_CHUNKS, dtype=np.uint64)
+    first = (count * c) // SIM_CHUNKS
+    end = np.minimum(count, (count * (c + 1)) // SIM_CHUNKS)
+    return first.astype(np.uint32), (end - first).astype(np.uint32)
+
+
+class VerifyLoad:
+    """One Processor's simulated signature load (worker/src/processor.rs:46-58 at spawn, :67-81
+    per batch) on the GPU.
+
+    At construction: ``keys`` keypairs from fresh seeds (OsRng in the reference; ``seed`` makes
+    them reproducible for tests), signatures over the 8-byte LE messages 0..keys-1 (``nw_sign_many``),
+    and one ``nw_committee_load`` of the public keys (their cache slots).  ``verify(batch)`` runs the
+    64 chunks of one batch as one ``nw_verify_batches`` call with fresh coefficients and raises
+    ``VerificationPanic`` when a chunk fails, as the reference's unwrap panics."""
+
+    def __init__(self, engine, keys: int = SIM_KEYS, seed=None):
+        import numpy as np
+        self.engine = engine
+        self.keys = keys
+        rng = np.random.default_rng(seed) if seed is not None else None
+        seeds = (rng.integers(0, 256, (keys, 32), dtype=np.uint8) if rng is not None
+                 else np.frombuffer(os.urandom(32 * keys), np.uint8).reshape(keys, 32))
+        self.msgs = np.arange(keys, dtype="<u8").view(np.uint8).reshape(keys, 8)   # i.to_le_bytes()
+        self.pks, self.sigs = engine.sign_many_np(seeds, self.msgs)
+        self.slots = engine.committee_load_np(self.pks)
+        self.verified = 0
+
+    def chunk_verdicts(self, count: int, zseed: bytes = None, batch_base: int = 0):
+        """batch_ok[64] of the first ``count`` signatures split as processor.rs:75-79 does."""
+        first, n = sim_chunks(count)
+        zseed = os.urandom(32) if zseed is None else zseed
+        batch_ok, _ = self.engine.verify_batches_np(first, n, self.msgs[:count], self.slots[:count],
+                                                    self.sigs[:count], zseed, batch_base)
+        return batch_ok
+
+    def verify(self, batch, zseed: bytes = None) -> int:
+        """The per-batch load of processor.rs:67-81; returns the number of signatures verified."""
+        ntx = batch_tx_count(batch)
+        if ntx < 0:
+            return 0
+        if ntx > self.keys:
+            warnings.warn("Batch size maximum for signature verification surpassed! %d" % ntx)
+        count = min(self.keys, ntx)
+        ok = self.chunk_verdicts(count, zseed)
+        if not ok.all():
+            raise VerificationPanic("verify_batch chunk(s) %s failed" % [i for i, v in enumerate(ok.tolist()) if not v])
+        self.verified += count
+        return count
 
 
 def serialize_worker_primary_message(digest32: bytes, worker_id: int, own_digest: bool) -> bytes:
@@ -112,14 +223,18 @@ class Processor:
     """worker/src/processor.rs ``Processor`` (digest, store, deliver) over a ``DigestBatcher``.
 
     ``run(batches)`` yields the serialized ``WorkerPrimaryMessage`` the reference sends on
-    ``tx_digest`` for each batch, in arrival order, after storing ``store[digest32] = batch``."""
+    ``tx_digest`` for each batch, in arrival order, after storing ``store[digest32] = batch``.
+    With ``verify`` (a ``VerifyLoad``: ``enable_verification``, processor.rs:43-58) every batch also
+    runs the simulated signature load when it arrives; a failing chunk raises ``VerificationPanic``
+    before that batch is stored or delivered, as the reference's unwrap panics the task."""
 
     def __init__(self, worker_id: int, own_digest: bool, store: Optional[MutableMapping] = None, engine=None,
-                 window: int = 64, depth: int = 2):
+                 window: int = 64, depth: int = 2, verify: Optional[VerifyLoad] = None):
         self.id = worker_id
         self.own_digest = own_digest
         self.store = store if store is not None else {}
         self.batcher = DigestBatcher(engine, window=window, depth=depth)
+        self.verify = verify
 
     def _deliver(self, items) -> Iterator[bytes]:
         for digest64, batch in items:
@@ -129,6 +244,14 @@ class Processor:
 
     def run(self, batches: Iterable) -> Iterator[bytes]:
         for b in batches:
+            if self.verify is not None:
+                try:
+                    self.verify.verify(b)
+                except VerificationPanic:
+                    # the reference's task had stored and delivered every earlier batch before it
+                    # panicked on this one: deliver what is in flight, then fail
+                    yield from self._deliver(self.batcher.drain())
+                    raise
             self.batcher.push(b)
             yield from self._deliver(self.batcher.ready())
         yield from self._deliver(self.batcher.drain())

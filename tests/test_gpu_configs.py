@@ -214,6 +214,109 @@ class TestC3C5:
         assert (stake == exp_stake).all()
 
 
+    def test_c5_rank_shards_match_one_call_and_oracle(self, c3):
+        """multi-rank verdict identity on the real engine.  The C5 classes (0.1%
+        signature-level classes plus the torsion committee keys, whose batch verdicts depend on z)
+        is cut into world = 2 and 8 rank shards exactly as shard.verify_sharded and bench.py cut it
+        (shard.partition, per-shard arrays, cert_base = global base + c0).  Each rank's shard runs
+        through the library on the host path (nw_verify_certs, shard.verify_shard) and on the
+        device path bench.py times (nw_verify_certs_dev with a status word); the concatenated
+        verdicts and stake equal the one-call result and the oracle, for two coefficient streams."""
+        import copy
+        import torch
+        from adversarial_mix import add_torsion_members, make_adversarial
+        from narwhal_amd import shard
+        eng, com0, slots0, cs0 = c3
+        cs = copy.copy(cs0)
+        com, _ = add_torsion_members(cs, com0, [17, 503], [42, 311, 777])
+        new_slots = eng.committee_load_np(com.pks[com0.size:], com.stake[com0.size:])
+        slots = np.concatenate([slots0, np.asarray(new_slots, slots0.dtype)])
+        # 0.1% signature-level classes (667 votes): about half the certificates stay clean, so the
+        # concatenated verdicts hold accepts, rejects and torsion-dependent verdicts side by side
+        make_adversarial(cs, com, 0.001, np.random.default_rng(23))
+        dev = torch.device("cuda", 0)
+        stream = torch.cuda.current_stream().cuda_stream
+        for base in (0, 7000):
+            one_ok, one_sig, one_stake = _verify(eng, cs, slots, ZSEED, base)
+            want = nw_ref.verify_certs(cs, com, list(range(cs.ncerts)), ZSEED, THREADS, cert_base=base)
+            assert one_ok.astype(bool).tolist() == want
+            assert 0 < sum(want) < cs.ncerts
+            for world in (2, 8):
+                h_ok, h_st, d_ok, d_st, d_strict = [], [], [], [], []
+                for rank in range(world):
+                    ranges, ok, st = shard.verify_shard(eng, cs, slots, ZSEED, rank, world, base)
+                    h_ok.append(ok)
+                    h_st.append(st)
+                    sh = shard.shard_inputs(cs, slots, rank, world, base)
+                    nc, ns = len(sh["n"]), len(sh["sigs"])
+                    o_ok = torch.zeros(nc, dtype=torch.uint8, device=dev)
+                    o_fl = torch.zeros(ns, dtype=torch.int32, device=dev)
+                    o_st = torch.zeros(nc, dtype=torch.int64, device=dev)
+                    status = torch.full((1,), 99, dtype=torch.int32, device=dev)
+                    t = {k: torch.from_numpy(np.ascontiguousarray(sh[k]).astype(dt)).to(dev)
+                         for k, dt in (("first", np.int32), ("n", np.int32), ("sigs", np.uint8),
+                                       ("signer_slots", np.int32), ("msgs", np.uint8))}
+                    eng.verify_certs_dev(nc, t["first"].data_ptr(), t["n"].data_ptr(), ns, t["sigs"].data_ptr(),
+                                         t["signer_slots"].data_ptr(), t["msgs"].data_ptr(), ZSEED, sh["cert_base"],
+                                         o_ok.data_ptr(), o_fl.data_ptr(), o_st.data_ptr(), stream,
+                                         d_status=status.data_ptr())
+                    torch.cuda.synchronize()
+                    assert int(status.item()) == 0
+                    d_ok.append(o_ok.cpu().numpy())
+                    d_st.append(o_st.cpu().numpy())
+                    d_strict.append((o_fl.cpu().numpy() & 0x8) != 0)
+                assert [r[1] - r[0] for r in ranges] == [len(x) for x in h_ok]
+                for got_ok, got_st in ((np.concatenate(h_ok), np.concatenate(h_st)),
+                                       (np.concatenate(d_ok), np.concatenate(d_st))):
+                    assert (got_ok == one_ok).all(), (base, world, np.flatnonzero(got_ok != one_ok)[:10])
+                    assert (got_st.astype(np.int64) == one_stake.astype(np.int64)).all(), (base, world)
+                assert (np.concatenate(d_strict) == one_sig.astype(bool)).all(), (base, world)
+
+    def test_split_batch_of_a_6667_vote_certificate(self, c3):
+        """VERDICT r04 item 2, split form: ONE 6,667-vote certificate (C4's 2f + 1) split over
+        world = 2 and 8 ranks by shard.split_bounds, each rank's row from shard.split_partial_row
+        (nw_verify_batch_partial, coefficients at the vote's global index), the verdict from
+        shard.split_verdict over the gathered rows (nw_points_sum_is_identity).  Honest, one
+        forged vote, and torsion-key votes whose verdict depends on z (eight batch indices): the
+        split verdict equals the one-call nw_verify_batch and the oracle every time."""
+        import copy
+        from adversarial_mix import add_torsion_members
+        from narwhal_amd import shard, workload
+        eng = c3[0]
+        com0 = workload.make_committee(6667, eng)   # not all cached (the C3 keys are its first 1,000): MSM path
+        cs0 = workload.make_certificates(com0, 1, 6667, eng)
+        msgs = [bytes(cs0.msgs[0])] * 6667
+        zseed = bytes(range(40, 72))
+
+        def case(cs, com, bi):
+            pks = [bytes(com.pks[k]) for k in cs.signer]
+            sigs = [bytes(x) for x in cs.sigs]
+            one = eng.verify_batch(msgs, pks, sigs, zseed, bi)
+            want = nw_ref.verify_batch_msgs(msgs, pks, sigs, zseed, bi)
+            assert one == want, bi
+            for world in (2, 8):
+                rows = [shard.split_partial_row(eng, msgs, pks, sigs, zseed, bi, r, world) for r in range(world)]
+                assert shard.split_verdict(eng, rows) == want, (bi, world)
+            return want
+
+        assert case(cs0, com0, 5) is True
+        forged = copy.copy(cs0)
+        forged.sigs = cs0.sigs.copy()
+        forged.sigs[3333] = np.frombuffer(nw_ref_sign_other(com0, cs0, 3333), np.uint8)
+        assert case(forged, com0, 5) is False
+        tors = copy.copy(cs0)
+        com_t, kinds = add_torsion_members(tors, com0, [], [100, 5000])   # A' = aB + jT8: z-dependent
+        assert len(kinds) == 2
+        verdicts = [case(tors, com_t, bi) for bi in range(8)]
+        print("torsion-key split verdicts over 8 batch indices:", verdicts)
+
+
+def nw_ref_sign_other(com, cs, i):
+    """Vote i re-signed over another message (class ix: valid encodings, wrong equation)."""
+    import ed25519_oracle as o
+    return o.sign(bytes(com.seeds[cs.signer[i]]), bytes(cs.msgs[0])[::-1])
+
+
 # ----------------------------------------------------------------------------- C4
 def test_c4_w12_sample_vs_oracle_and_localized():
     eng = _engine()

@@ -178,6 +178,40 @@ def test_overlapping_ranges_are_arg_errors(engine, keys):
                                                       _expect(m0, pks[4:6], s0[4:6], 1)]
 
 
+def test_overlapping_device_ranges_reject_both_certificates(engine, keys):
+    """with a device status word the kernels still run on overlapping ranges.
+    Votes 0-3 sign m0 (certificate 0 = votes [0, 4)), votes 4-5 sign m1 (certificate 1 = votes
+    [2, 6) over m1): votes 2 and 3 are claimed twice, and whichever certificate the vote map ends
+    with checks them against ITS message.  Whatever that order, both certificates are rejected and
+    neither is credited stake of a vote it does not own."""
+    import torch
+    rng, seeds, pks, slots = keys
+    m0 = bytes(rng.randrange(256) for _ in range(32))
+    m1 = bytes(rng.randrange(256) for _ in range(32))
+    sigs = [o.sign(seeds[v], m0 if v < 4 else m1) for v in range(6)]
+    dev = torch.device("cuda", 0)
+    d_first = torch.tensor([0, 2], dtype=torch.int32, device=dev)
+    d_n = torch.tensor([4, 4], dtype=torch.int32, device=dev)
+    d_sig = torch.from_numpy(np.frombuffer(b"".join(sigs), np.uint8).copy()).to(dev)
+    d_signer = torch.tensor(slots[:6], dtype=torch.int32, device=dev)
+    d_msg = torch.from_numpy(np.frombuffer(m0 + m1, np.uint8).copy()).to(dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    for rep in range(8):   # the atomic order of the vote map may differ from launch to launch
+        ok = torch.full((2,), 7, dtype=torch.uint8, device=dev)
+        stake = torch.full((2,), -1, dtype=torch.int64, device=dev)
+        status = torch.full((1,), 99, dtype=torch.int32, device=dev)
+        engine.verify_certs_dev(2, d_first.data_ptr(), d_n.data_ptr(), 6, d_sig.data_ptr(), d_signer.data_ptr(),
+                                d_msg.data_ptr(), ZSEED, 0, ok.data_ptr(), 0, stake.data_ptr(), stream,
+                                d_status=status.data_ptr())
+        torch.cuda.synchronize()
+        assert int(status.item()) == 2, rep
+        assert ok.cpu().tolist() == [0, 0], rep
+        st = stake.cpu().tolist()
+        # stake 1 per key.  Certificate 0 owns votes 0-1 for sure and 2-3 if it won them (they match
+        # m0); certificate 1 owns 4-5 (match m1) and may own 2-3, which never match m1
+        assert 2 <= st[0] <= 4 and st[1] == 2, (rep, st)
+
+
 @pytest.mark.parametrize("sh", [1, 2, 3])
 def test_sha512_unaligned_padding_block_ends_flush(engine, sh):
     """Messages at an odd offset whose length mod 128 >= 112 (the padding needs a second block),

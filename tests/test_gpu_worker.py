@@ -102,3 +102,78 @@ def test_async_window_above_parallel_staging_threshold(engine):
     assert sum(len(m) for m in msgs) > 32 << 20
     got = engine.sha512_many_submit(msgs).wait()
     assert got == [hashlib.sha512(bytes(m)).digest() for m in msgs]
+
+
+def test_worker_spawn_sequence_two_processors_cached():
+    """INTEGRATION.md §3, the worker process exactly as documented:
+    * the engine is created in committee mode with both Processors' simulation keys declared
+      (``worker_engine``: max_keys 200,000); Worker::spawn loads NO committee;
+    * Processor::spawn for our batches (worker/src/worker.rs:182), then for others' batches (:228):
+      each makes 100,000 keypairs, signs the LE messages 0..99,999 and loads its keys
+      (processor.rs:46-58); the second load must not hit NW_ERR_NOMEM;
+    * per batch: min(100,000, #tx) signatures in 64 verify_batch chunks (processor.rs:67-81) as ONE
+      nw_verify_batches call on the cached combs.  Chunk verdicts against the C restatement of
+      dalek (oracle/nw_ref.c) with the same coefficients, including chunks with a corrupted
+      signature; a 100,001-transaction batch verifies the full 100,000; ``Processor`` with the load
+      delivers every batch's digest."""
+    import nw_ref
+    from narwhal_amd import workload, worker as w
+    eng = w.worker_engine(device=0)
+    try:
+        own = w.VerifyLoad(eng, seed=5)       # Processor::spawn(.., own_digest = true, ..)
+        others = w.VerifyLoad(eng, seed=6)    # Processor::spawn(.., own_digest = false, ..)
+        assert eng.committee_size() == 2 * w.SIM_KEYS
+        assert eng.key_window() in (8, 9), eng.key_window()
+        print("worker engine: window W%d for %d keys" % (eng.key_window(), eng.committee_size()))
+        assert not np.array_equal(own.pks[:8], others.pks[:8])
+
+        def oracle_chunks(load, count, zseed, base, only=None):
+            first, n = w.sim_chunks(count)
+            want = []
+            for c in range(64):
+                if only is not None and c not in only:
+                    want.append(None)
+                    continue
+                f, k = int(first[c]), int(n[c])
+                want.append(nw_ref.verify_batch_msgs([bytes(m) for m in load.msgs[f:f + k]],
+                                                     [bytes(p) for p in load.pks[f:f + k]],
+                                                     [bytes(s) for s in load.sigs[f:f + k]], zseed, base + c))
+            return want
+
+        zseed = bytes(range(7, 39))
+        for load in (own, others):                       # a C4-shape batch: 977 transactions
+            got = load.chunk_verdicts(977, zseed, 0).astype(bool).tolist()
+            assert got == oracle_chunks(load, 977, zseed, 0) == [True] * 64
+        # corrupted signatures in three chunks of our Processor's load (a bit of R, S + l, another message)
+        saved = own.sigs.copy()
+        try:
+            own.sigs[100, 3] ^= 0x10
+            sv = int.from_bytes(bytes(own.sigs[500, 32:]), "little") + (2 ** 252 + 27742317777372353535851937790883648493)
+            own.sigs[500, 32:] = np.frombuffer(sv.to_bytes(32, "little"), np.uint8)
+            own.sigs[900] = others.sigs[900]
+            got = own.chunk_verdicts(977, zseed, 64).astype(bool).tolist()
+            want = oracle_chunks(own, 977, zseed, 64)
+            assert got == want
+            first, n = w.sim_chunks(977)
+            hit = sorted({c for i in (100, 500, 900) for c in range(64) if first[c] <= i < first[c] + n[c]})
+            assert [c for c in range(64) if not got[c]] == hit and len(hit) == 3
+            with pytest.raises(w.VerificationPanic):
+                own.verify(workload.worker_batch(977, 512))
+        finally:
+            own.sigs[:] = saved
+        # a batch above the simulation maximum: the first 100,000 signatures (processor.rs:70-73)
+        big = workload.worker_batch(w.SIM_KEYS + 1, 9)
+        with pytest.warns(UserWarning, match="maximum"):
+            assert others.verify(big) == w.SIM_KEYS
+        got = others.chunk_verdicts(w.SIM_KEYS, zseed, 1000).astype(bool).tolist()
+        assert got == [True] * 64
+        want = oracle_chunks(others, w.SIM_KEYS, zseed, 1000, only={0, 31, 63})
+        assert [want[0], want[31], want[63]] == [True] * 3
+        # the Processor loop with the load enabled: digests as the reference's hash_and_store
+        batches = [workload.worker_batch(977, 512, b) for b in range(3)] + [workload.worker_batch(10, 32, 9)]
+        p = w.Processor(worker_id=2, own_digest=True, engine=eng, window=2, depth=2, verify=own)
+        out = list(p.run(batches))
+        assert [m[4:36] for m in out] == [hashlib.sha512(b).digest()[:32] for b in batches]
+        assert own.verified == 3 * 977 + 10
+    finally:
+        eng.close()

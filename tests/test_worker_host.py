@@ -124,3 +124,67 @@ def test_bad_parameters():
         w.DigestBatcher(FakeEngine(), window=0)
     with pytest.raises(ValueError):
         w.DigestBatcher(FakeEngine(), depth=0)
+
+
+# ----------------------------------------------------------------------- simulated verify load (A13)
+def test_batch_tx_count_parses_worker_messages():
+    """worker/src/processor.rs:68-70: bincode WorkerMessage; Batch -> its transaction count,
+    BatchRequest -> not verified, malformed -> error (the reference's unwrap panics)."""
+    from narwhal_amd import workload
+    w = _import()
+    assert w.batch_tx_count(workload.worker_batch(977, 512)) == 977
+    assert w.batch_tx_count(workload.worker_batch(0, 512)) == 0
+    assert w.batch_tx_count(workload.worker_batch(5, 9)) == 5
+    req = struct.pack("<IQ", 1, 0) + struct.pack("<Q", 32) + b"k" * 32   # BatchRequest(vec![], origin)
+    assert w.batch_tx_count(req) == -1
+    good = workload.worker_batch(3, 16)
+    for bad in (good[:-1], good[:10], b"\x02\0\0\0", b""):
+        with pytest.raises(ValueError):
+            w.batch_tx_count(bad)
+
+
+@pytest.mark.parametrize("count", [0, 1, 63, 64, 977, 100_000])
+def test_sim_chunks_match_reference_split(count):
+    """processor.rs:75-77: chunk c = [count*c/64, min(count, count*(c+1)/64)) in integer arithmetic;
+    the chunks tile [0, count) in order."""
+    w = _import()
+    first, n = w.sim_chunks(count)
+    want = [((count * c) // 64, min(count, (count * (c + 1)) // 64)) for c in range(64)]
+    assert [(int(f), int(f + k)) for f, k in zip(first, n)] == want
+    assert int(n.sum()) == count
+
+
+class _FakeLoad:
+    """Stand-in VerifyLoad: fails on the batches whose index is in ``bad``."""
+
+    def __init__(self, w, bad=()):
+        self.w, self.bad, self.seen = w, set(bad), []
+
+    def verify(self, batch):
+        w = self.w
+        i = len(self.seen)
+        self.seen.append(w.batch_tx_count(batch))
+        if i in self.bad:
+            raise w.VerificationPanic("chunk 0 failed")
+        return self.seen[-1]
+
+
+def test_processor_runs_verify_load_and_delivers_before_panic():
+    """Every batch runs the simulated load on arrival; a failing batch raises after every earlier
+    batch was stored and delivered, and is itself neither stored nor delivered (the reference's
+    task panics at the unwrap, processor.rs:78, before :84)."""
+    from narwhal_amd import workload
+    w = _import()
+    batches = [workload.worker_batch(4, 16, b) for b in range(5)]
+    load = _FakeLoad(w)
+    p = w.Processor(worker_id=1, own_digest=True, engine=FakeEngine(), window=2, depth=2, verify=load)
+    out = list(p.run(batches))
+    assert len(out) == 5 and load.seen == [4] * 5
+    load = _FakeLoad(w, bad={3})
+    p = w.Processor(worker_id=1, own_digest=True, engine=FakeEngine(), window=2, depth=2, verify=load)
+    got = []
+    with pytest.raises(w.VerificationPanic):
+        for m in p.run(batches):
+            got.append(m)
+    assert len(got) == 3 and len(p.store) == 3
+    assert set(p.store) == {hashlib.sha512(b).digest()[:32] for b in batches[:3]}

@@ -1,7 +1,7 @@
 """Clock-normalised roofline fraction of k_verify.
 
 Both the v_mad_u64_u32 peak (tools/valu_peak) and k_verify ran under one rocprofv3 PMC pass with
-GRBM_GUI_ACTIVE (tools/r04_pmc.sh), so each is known in shader cycles, not only in wall time:
+GRBM_GUI_ACTIVE (one PMC pass each, tools/gpu_pmc.sh), so each is known in shader cycles, not only in wall time:
   peak_per_cycle = v_mad_u64_u32 lane-ops of the microbenchmark / its GPU cycles
   kverify        = algorithmic MADs per launch (162 FM x 100 per signature at C2) / its GPU cycles
   frac_per_cycle = kverify / peak_per_cycle     (independent of the clock either kernel ran at)
