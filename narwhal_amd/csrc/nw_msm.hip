@@ -23,6 +23,12 @@
 #include "nw_msm.h"
 #include "nw_quad.h"
 
+// Built as three objects (Makefile: -DNW_MSM_PART=7 / 8 / 0) so the two bucket-width instantiations
+// and the rest compile in parallel: one object holding all of them took ~8 minutes.
+#ifndef NW_MSM_PART
+#define NW_MSM_PART 0
+#endif
+
 namespace nw {
 
 // ------------------------------------------------------------------------------------ helpers
@@ -573,6 +579,7 @@ __global__ void __launch_bounds__(64) k_msm_final(MsmParams a, const uint32_t* w
 }
 
 // Sum of npts extended points (the shards of one split batch) == identity.
+#if NW_MSM_PART == 0
 __global__ void __launch_bounds__(64) k_points_identity(uint32_t npts, const uint32_t* pts, uint8_t* out) {
     // lanes stride over the points, then a shuffle tree (all values in VGPRs)
     const uint32_t L = threadIdx.x;
@@ -582,9 +589,10 @@ __global__ void __launch_bounds__(64) k_points_identity(uint32_t npts, const uin
     for (unsigned off = 32; off > 0; off >>= 1) acc = ge_add_p3(acc, ge_shfl_down(acc, off));
     if (L == 0) out[0] = ge_is_identity(acc) ? 1 : 0;
 }
+#endif
 
 template <int C>
-static hipError_t launch_msm_c(const MsmParams& p, hipStream_t st) {
+hipError_t launch_msm_c(const MsmParams& p, hipStream_t st) {
     hipError_t e = hipSuccess;
     // no signatures (an empty shard of a split batch, counts all 0): the bad flags are zeroed by
     // the metadata upload and no zs column is read, so wsum/final give the identity -> Ok, as
@@ -610,6 +618,12 @@ static hipError_t launch_msm_c(const MsmParams& p, hipStream_t st) {
     return hipGetLastError();
 }
 
+#if NW_MSM_PART == 7 || NW_MSM_PART == 8
+template hipError_t launch_msm_c<NW_MSM_PART>(const MsmParams&, hipStream_t);
+#else
+extern template hipError_t launch_msm_c<7>(const MsmParams&, hipStream_t);
+extern template hipError_t launch_msm_c<8>(const MsmParams&, hipStream_t);
+
 hipError_t launch_msm(const MsmParams& p, hipStream_t st) {
     if (p.nb == 0) return hipSuccess;
     switch (p.c) {
@@ -632,5 +646,6 @@ hipError_t launch_verify_var(const VerifyParams& p, int msgmode, uint32_t* scrat
     else hipLaunchKernelGGL(k_verify_var<false>, dim3(blocks_for(p.gn, 256)), dim3(256), 0, st, p, scratch);
     return hipGetLastError();
 }
+#endif  // NW_MSM_PART
 
 }  // namespace nw
