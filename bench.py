@@ -39,6 +39,7 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+
 METRIC = "Ed25519 sigs verified/s (node, 1/2/4/8 GPU); p50 latency per 2f+1 certificate"
 # SURVEY.md §8(d) cost model v1 (frozen): FM per signature of dalek's algorithm at n votes per
 # certificate (Straus / Pippenger MSM + R decompression).  Reported as ``dalek_equiv`` only: the
@@ -301,6 +302,81 @@ def host_fed(eng, cs, slots, zseed, chunks=8, threads=4, reps=5):
                     "fresh_buffers: each pass on newly allocated host arrays" % (chunks, threads, reps)}
 
 
+class BatchUploader:
+    """C4 with host-resident worker batches (``--batches host``, the default): each step's batches come from
+    PAGEABLE host memory, as the worker's Processor receives them (worker/src/processor.rs:63-65).
+    ``stage_next`` copies them into one of two pinned buffers with ``threads`` host threads, chunk by
+    chunk, and enqueues each chunk's DMA into one of two HBM buffers on a copy stream as soon as the
+    chunk is staged; the digests of step i read the buffer step i-1 uploaded (double buffering, as the
+    worker's DigestBatcher keeps DEPTH = 2 windows in flight).  Host staging, PCIe and the digests
+    are all inside the timed loop."""
+
+    def __init__(self, host_b, dev, threads=8, chunk=32 << 20, nbuf=2):
+        import torch
+        from concurrent.futures import ThreadPoolExecutor
+        self.host = host_b.reshape(-1)
+        self.n = self.host.shape[0]
+        self.chunk = chunk
+        self.nbuf = nbuf
+        self.pinned = [torch.empty(self.n, dtype=torch.uint8).pin_memory() for _ in range(nbuf)]
+        self.pinned_np = [p.numpy() for p in self.pinned]
+        self.dev_buf = [torch.empty(self.n, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+        self.copy_stream = torch.cuda.Stream(device=dev)
+        self.ev_up = [torch.cuda.Event() for _ in range(nbuf)]
+        self.ev_read = [None] * nbuf       # last digest launch that read dev_buf[j]
+        self.pool = ThreadPoolExecutor(threads)
+        self.threads = threads
+        self.next = 0                      # buffer the next stage_next fills
+        self.stage_s = []
+        self.trace = []                    # (buffer, start, wait for the previous DMA, stage + enqueue)
+
+    def _copy(self, j, a, b):
+        import numpy as np
+        np.copyto(self.pinned_np[j][a:b], self.host[a:b])
+
+    def stage_next(self, read_stream):
+        """Stage + upload the next step's batches into buffer self.next.  ``read_stream``: the stream
+        on which this step's digests (reading the other buffer) were just launched, or None."""
+        import torch
+        if read_stream is not None:       # a FRESH event per record: the reader of each buffer
+            ev = torch.cuda.Event()
+            ev.record(read_stream)
+            self.ev_read[self.pending] = ev
+        j = self.next
+        t0 = time.perf_counter()
+        self.ev_up[j].synchronize()        # the previous DMA out of pinned[j] is done
+        t1 = time.perf_counter()
+        if self.ev_read[j] is not None:
+            self.copy_stream.wait_event(self.ev_read[j])   # the digests that read dev_buf[j] are done
+        bounds = list(range(0, self.n, self.chunk)) + [self.n]
+        futs = [self.pool.submit(self._copy, j, a, b) for a, b in zip(bounds, bounds[1:])]
+        with torch.cuda.stream(self.copy_stream):
+            for f, a, b in zip(futs, bounds, bounds[1:]):
+                f.result()
+                self.dev_buf[j][a:b].copy_(self.pinned[j][a:b], non_blocking=True)
+        self.ev_up[j].record(self.copy_stream)
+        t2 = time.perf_counter()
+        self.stage_s.append(t2 - t0)
+        self.trace.append((j, t0, t1 - t0, t2 - t1))
+        self.pending = j
+        self.next = (j + 1) % self.nbuf
+
+    def ready_buffer(self, stream):
+        """The buffer the last stage_next uploaded, ordered after its upload on ``stream``."""
+        stream.wait_event(self.ev_up[self.pending])
+        return self.dev_buf[self.pending]
+
+    def stats(self):
+        st = sorted(self.stage_s[1:]) or [0.0]
+        t0 = self.trace[0][1] if self.trace else 0.0
+        return {"host_threads": self.threads, "chunk_MiB": self.chunk >> 20,
+                "stage_and_enqueue_ms_p50": st[len(st) // 2] * 1e3,
+                "trace_ms": [[j, round((t - t0) * 1e3, 2), round(w * 1e3, 2), round(c * 1e3, 2)]
+                             for j, t, w, c in self.trace[-12:]],
+                "note": "host time per step to copy %d MB from pageable into pinned memory (the DMAs overlap it "
+                        "chunk by chunk)" % (self.n // 10 ** 6)}
+
+
 def digest_leg(eng, dev, n_node, n_share, reps, cpu_seconds, verify_step):
     """Worker batch digests (worker/src/processor.rs:65), one lane per batch (each batch is one
     sequential SHA-512 compression chain)."""
@@ -555,6 +631,17 @@ def parse_args(argv):
                          "(r04p) but the timed k_verify launches then overlap each other and the roofline "
                          "measures shared time (frac 0.40-0.45 instead of ~0.47); 1 for C4, where two 8.3M-signature "
                          "k_verify launches over 10,000 key tables slow each other down (r04o: 401 vs 466 M sigs/s)")
+    ap.add_argument("--batches", choices=("host", "hbm"), default="host",
+                    help="C4: where the worker batches start each step.  host (default): in pageable host memory, "
+                         "as the Processor receives them (worker/src/processor.rs:63-65); host threads stage them "
+                         "into pinned buffers and DMA them to HBM inside the timed loop (step i hashes what step "
+                         "i-1 uploaded while it stages and uploads step i+1's batches).  hbm: resident in HBM "
+                         "(round 4's C4 line, PCIe excluded)")
+    ap.add_argument("--digest-join", action="store_true",
+                    help="C4: end every step when its digests end (round 4's structure).  Default: the digests "
+                         "of consecutive steps overlap (two alternating high-priority digest streams; step i+1's "
+                         "digests start when step i's verify kernels end), so a batch's serial SHA-512 chain "
+                         "bounds its latency but not the step")
     ap.add_argument("--key-window", type=int, default=-1,
                     help="key comb window; -1 = committee mode (library sizes it for the loaded committee)")
     ap.add_argument("--dry-run", action="store_true",
@@ -703,6 +790,15 @@ def latency_legs(eng, com, slots, cs, samples):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
+    if CONFIGS[args.config]["digest_batches"] and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
+        # HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default).
+        # Streams that share a queue share its in-order execution: at C4 the batch upload's copy
+        # stream sat behind a digest kernel on another stream and the steps serialized (25.1 vs 20.6
+        # ms per step with 16 queues, profiles/r05/c4_hwq_r05.txt).  Only the multi-stream C4 step
+        # gets 16: the one-stream C2 step ran 3.1 instead of 1.36 ms per step with them (host-side
+        # cost per call, the GPU idle between steps).  Set before anything initializes HIP; the rank
+        # processes launched below inherit it.
+        os.environ["GPU_MAX_HW_QUEUES"] = "16"
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args, argv)
     if args.dry_run:
@@ -757,17 +853,25 @@ def main(argv=None):
     # C4: the rank's worker-batch digests (worker/src/processor.rs:65) run inside the timed step on
     # a second stream, concurrently with the verify kernels; the step ends when both are done
     ndig = plan["digest_batches"]
+    from_host = bool(ndig) and args.batches == "host"
+    pipelined = bool(ndig) and not args.digest_join
     if ndig:
         import hashlib
         host_b = workload.worker_batches_np(ndig)
         blen = host_b.shape[1]
-        d_bdata = torch.from_numpy(host_b.reshape(-1)).to(dev)
+        if from_host:
+            uploader = BatchUploader(host_b, dev, nbuf=3 if pipelined else 2)
+            d_bdata = None
+        else:
+            d_bdata = torch.from_numpy(host_b.reshape(-1)).to(dev)
         d_boff = torch.arange(ndig, dtype=torch.int64, device=dev) * blen
         d_blen = torch.full((ndig,), blen, dtype=torch.int64, device=dev)
-        d_bouts = [torch.empty((ndig, 64), dtype=torch.uint8, device=dev) for _ in range(nst)]
-        # one digest stream per batch in flight: step i's digests overlap step i + 1's
-        s_digs = [torch.cuda.Stream(device=dev) for _ in range(nst)]
-        ev_digs = [torch.cuda.Event() for _ in range(nst)]
+        # joined: one digest stream per batch in flight.  Pipelined: two alternating digest streams
+        # at high priority (step i + 1's digests run beside the tail of step i's), each with its output
+        ndst = 2 if pipelined else nst
+        d_bouts = [torch.empty((ndig, 64), dtype=torch.uint8, device=dev) for _ in range(ndst)]
+        s_digs = [torch.cuda.Stream(device=dev, priority=-1 if pipelined else 0) for _ in range(ndst)]
+        ev_digs = [torch.cuda.Event() for _ in range(ndst)]
 
     # N > 1: every all_gather on one stream (collectives of one communicator stay serialized), after
     # its batch's kernels; a stream reuses its output set only after that set's all_gather
@@ -785,38 +889,71 @@ def main(argv=None):
             # 486-491 M sigs/s, r04r: a digest launched while k_verify holds every CU waits for CUs;
             # two alternating digest streams without the join, 460 M, r04u: the second stream's digest
             # still started only when the first finished, then waited for CUs.)
-            s_dig, ev_dig = s_digs[i % nst], ev_digs[i % nst]
+            di = i % len(s_digs)
+            s_dig, ev_dig = s_digs[di], ev_digs[di]
+            # after the previous step's verify kernels: a digest enqueued while k_verify holds every
+            # CU would wait for whole CUs to drain (its workgroups take a CU each)
             s_dig.wait_stream(cur)
-            eng.sha512_many_dev(d_bdata.data_ptr(), d_boff.data_ptr(), d_blen.data_ptr(), ndig,
-                                d_bouts[i % nst].data_ptr(), s_dig.cuda_stream)
+            if from_host:
+                src = uploader.ready_buffer(s_dig)         # uploaded during the previous step
+            else:
+                src = d_bdata
+            eng.sha512_many_dev(src.data_ptr(), d_boff.data_ptr(), d_blen.data_ptr(), ndig,
+                                d_bouts[di].data_ptr(), s_dig.cuda_stream)
             ev_dig.record(s_dig)
         verify_step(cur, o)
-        if ndig:
+        if from_host:
+            # host threads stage the NEXT step's batches into pinned memory and DMA them while this
+            # step's kernels run (the next step's digests wait for that upload; the timed region's
+            # closing synchronize waits for every upload)
+            uploader.stage_next(read_stream=s_dig)
+        if ndig and not pipelined:
             cur.wait_event(ev_dig)
         if world > 1:
             # RCCL all_gathers of the verdict bitmaps + stake and (C4) of the ranks' worker digests
-            # (32 B per batch), after this step's kernels (cur has waited for the digests above)
+            # (32 B per batch), after this step's kernels.  Pipelined: the digests all-gathered in
+            # step i are step i - 1's (finished while step i verified); the last step's after the loop
+            dig_out = None
+            if ndig and not pipelined:
+                dig_out = d_bouts[i % len(d_bouts)]
+            elif ndig and i > 0:
+                dig_out = d_bouts[(i - 1) % len(d_bouts)]
+                cur.wait_event(ev_digs[(i - 1) % len(ev_digs)])
             if s_comm is None:
-                if ndig:
-                    shard.allgather_digests(d_bouts[i % nst])
+                if dig_out is not None:
+                    shard.allgather_digests(dig_out)
                 shard.allgather_verdicts(o["ok"], o["stake"], ranges)
             else:
                 s_comm.wait_stream(cur)
                 with torch.cuda.stream(s_comm):
-                    if ndig:
-                        shard.allgather_digests(d_bouts[i % nst])
+                    if dig_out is not None:
+                        shard.allgather_digests(dig_out)
                     shard.allgather_verdicts(o["ok"], o["stake"], ranges)
                 cur.wait_stream(s_comm)
 
+    def drain_digests():
+        """Pipelined C4: the last step's digests (and, N > 1, their all-gather) inside the timed region."""
+        if not pipelined:
+            return
+        i = n_step[0] - 1
+        cur = streams[i % nst]
+        cur.wait_event(ev_digs[i % len(ev_digs)])
+        if world > 1:
+            shard.allgather_digests(d_bouts[i % len(d_bouts)])
+
+    if from_host:
+        uploader.stage_next(read_stream=None)   # the first step's batches
     torch.cuda.synchronize()       # inputs resident before any stream reads them
     for _ in range(args.warmup):
         step()
+    if ndig:
+        drain_digests()
     torch.cuda.synchronize()
     ok_all = all(bool(o["ok"].all().item()) and bool((o["stake"] == plan["votes"]).all().item())
                  and int(o["status"].item()) == 0 for o in outs[:min(nst, max(1, args.warmup))])
     if ndig:
         for b in (0, ndig - 1):
-            for d_bout in d_bouts[:min(nst, max(1, args.warmup))]:
+            for d_bout in d_bouts[:min(len(d_bouts), max(1, args.warmup))]:
                 ok_all = ok_all and bytes(d_bout[b].cpu().numpy()) == hashlib.sha512(host_b[b].tobytes()).digest()
     if world > 1:
         dist.barrier()
@@ -828,6 +965,8 @@ def main(argv=None):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    if ndig:
+        drain_digests()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -909,6 +1048,9 @@ def main(argv=None):
                             "per node round, partitioned over the GPUs" if strong else "per GPU"))
         if ndig:
             workload_desc += " + %d worker-batch SHA-512 digests (%d B each) per GPU on a second stream" % (ndig, blen)
+            if from_host:
+                workload_desc += (", batches from pageable host memory (staged to pinned + H2D inside the timed "
+                                  "loop, double-buffered)")
         out = {
             "metric": METRIC, "value": value, "unit": "sigs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -924,7 +1066,10 @@ def main(argv=None):
         }
         if ndig:
             out["digest_in_step"] = {"batches_per_gpu": ndig, "bytes_per_gpu_per_step": ndig * blen,
-                                     "GBps_per_gpu": ndig * blen * args.steps / elapsed / 1e9}
+                                     "GBps_per_gpu": ndig * blen * args.steps / elapsed / 1e9,
+                                     "batches_from_host": from_host}
+            if from_host:
+                out["digest_in_step"]["upload"] = uploader.stats()
         # GPU legs first: the CPU baselines run more threads than the container's CPU quota, and the
         # cgroup throttling that follows would slow the host side of the next leg
         c2 = args.config == "C2"
