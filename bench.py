@@ -311,7 +311,7 @@ class BatchUploader:
     worker's DigestBatcher keeps DEPTH = 2 windows in flight).  Host staging, PCIe and the digests
     are all inside the timed loop."""
 
-    def __init__(self, host_b, dev, threads=8, chunk=32 << 20, nbuf=2):
+    def __init__(self, host_b, dev, threads=8, chunk=32 << 20, nbuf=2, copy_streams=None):
         import torch
         from concurrent.futures import ThreadPoolExecutor
         self.host = host_b.reshape(-1)
@@ -321,7 +321,11 @@ class BatchUploader:
         self.pinned = [torch.empty(self.n, dtype=torch.uint8).pin_memory() for _ in range(nbuf)]
         self.pinned_np = [p.numpy() for p in self.pinned]
         self.dev_buf = [torch.empty(self.n, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
-        self.copy_stream = torch.cuda.Stream(device=dev)
+        # copy_streams[j]: the stream buffer j's DMAs go on.  Given the digest streams (one per buffer),
+        # each upload is queued behind the digests that last read its buffer and ahead of the digests
+        # that will read it, so stream order alone orders them and no other stream (which HIP may map
+        # onto the same in-order hardware queue) is involved
+        self.copy_streams = copy_streams or [torch.cuda.Stream(device=dev)] * nbuf
         self.ev_up = [torch.cuda.Event() for _ in range(nbuf)]
         self.ev_read = [None] * nbuf       # last digest launch that read dev_buf[j]
         self.pool = ThreadPoolExecutor(threads)
@@ -346,15 +350,16 @@ class BatchUploader:
         t0 = time.perf_counter()
         self.ev_up[j].synchronize()        # the previous DMA out of pinned[j] is done
         t1 = time.perf_counter()
+        cs = self.copy_streams[j]
         if self.ev_read[j] is not None:
-            self.copy_stream.wait_event(self.ev_read[j])   # the digests that read dev_buf[j] are done
+            cs.wait_event(self.ev_read[j])   # the digests that read dev_buf[j] are done
         bounds = list(range(0, self.n, self.chunk)) + [self.n]
         futs = [self.pool.submit(self._copy, j, a, b) for a, b in zip(bounds, bounds[1:])]
-        with torch.cuda.stream(self.copy_stream):
+        with torch.cuda.stream(cs):
             for f, a, b in zip(futs, bounds, bounds[1:]):
                 f.result()
                 self.dev_buf[j][a:b].copy_(self.pinned[j][a:b], non_blocking=True)
-        self.ev_up[j].record(self.copy_stream)
+        self.ev_up[j].record(cs)
         t2 = time.perf_counter()
         self.stage_s.append(t2 - t0)
         self.trace.append((j, t0, t1 - t0, t2 - t1))
@@ -642,6 +647,7 @@ def parse_args(argv):
                          "of consecutive steps overlap (two alternating high-priority digest streams; step i+1's "
                          "digests start when step i's verify kernels end), so a batch's serial SHA-512 chain "
                          "bounds its latency but not the step")
+    ap.add_argument("--hw-queues", type=int, default=0, help="set GPU_MAX_HW_QUEUES (<= 32) before HIP starts")
     ap.add_argument("--key-window", type=int, default=-1,
                     help="key comb window; -1 = committee mode (library sizes it for the loaded committee)")
     ap.add_argument("--dry-run", action="store_true",
@@ -790,15 +796,12 @@ def latency_legs(eng, com, slots, cs, samples):
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     args = parse_args(argv)
-    if CONFIGS[args.config]["digest_batches"] and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 16:
-        # HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default).
-        # Streams that share a queue share its in-order execution: at C4 the batch upload's copy
-        # stream sat behind a digest kernel on another stream and the steps serialized (25.1 vs 20.6
-        # ms per step with 16 queues, profiles/r05/c4_hwq_r05.txt).  Only the multi-stream C4 step
-        # gets 16: the one-stream C2 step ran 3.1 instead of 1.36 ms per step with them (host-side
-        # cost per call, the GPU idle between steps).  Set before anything initializes HIP; the rank
-        # processes launched below inherit it.
-        os.environ["GPU_MAX_HW_QUEUES"] = "16"
+    if args.hw_queues:
+        # HIP multiplexes a process's streams onto GPU_MAX_HW_QUEUES in-order hardware queues (4 by
+        # default).  Left at 4: with 16 a C2 step ran 3.1 instead of 1.36 ms (stalls of ~14 ms between
+        # steps, the GPU idle) and C4 434 instead of 575 M sigs/s (profiles/r05/c4_hwq_r05.txt); the
+        # C4 step instead keeps each upload on the stream of the digests that read it.
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         return launch_ranks(args, argv)
     if args.dry_run:
@@ -859,24 +862,26 @@ def main(argv=None):
         import hashlib
         host_b = workload.worker_batches_np(ndig)
         blen = host_b.shape[1]
-        if from_host:
-            uploader = BatchUploader(host_b, dev, nbuf=3 if pipelined else 2)
-            d_bdata = None
-        else:
-            d_bdata = torch.from_numpy(host_b.reshape(-1)).to(dev)
         d_boff = torch.arange(ndig, dtype=torch.int64, device=dev) * blen
         d_blen = torch.full((ndig,), blen, dtype=torch.int64, device=dev)
         # joined: one digest stream per batch in flight.  Pipelined: two alternating digest streams
         # at high priority (step i + 1's digests run beside the tail of step i's), each with its output
+        # and, with host batches, its upload buffer (step i's batches are DMA'd on step i's digest stream)
         ndst = 2 if pipelined else nst
         d_bouts = [torch.empty((ndig, 64), dtype=torch.uint8, device=dev) for _ in range(ndst)]
         s_digs = [torch.cuda.Stream(device=dev, priority=-1 if pipelined else 0) for _ in range(ndst)]
         ev_digs = [torch.cuda.Event() for _ in range(ndst)]
+        if from_host:
+            uploader = BatchUploader(host_b, dev, nbuf=2, copy_streams=s_digs if pipelined else None)
+            d_bdata = None
+        else:
+            d_bdata = torch.from_numpy(host_b.reshape(-1)).to(dev)
 
     # N > 1: every all_gather on one stream (collectives of one communicator stay serialized), after
     # its batch's kernels; a stream reuses its output set only after that set's all_gather
     s_comm = torch.cuda.Stream(device=dev) if world > 1 and nst > 1 else None
     n_step = [0]
+    ev_pre = [None]
 
     def step():
         i = n_step[0]
@@ -891,9 +896,18 @@ def main(argv=None):
             # still started only when the first finished, then waited for CUs.)
             di = i % len(s_digs)
             s_dig, ev_dig = s_digs[di], ev_digs[di]
-            # after the previous step's verify kernels: a digest enqueued while k_verify holds every
-            # CU would wait for whole CUs to drain (its workgroups take a CU each)
-            s_dig.wait_stream(cur)
+            # Joined: after the previous step's verify kernels (a digest enqueued while k_verify holds
+            # every CU waits for whole CUs to drain: its workgroups take a CU each).  Pipelined: only
+            # after its own stream's earlier work (step i-2's digests, this step's upload), so it is
+            # queued while step i-1's k_verify still runs and takes CUs as that grid's dispatch ends,
+            # ahead of step i's k_verify (which waits for step i-1's k_finish); when both became ready
+            # at the same event, the verify grid won the CUs in about one run in three and the digests
+            # ran 26.7 instead of 16-17 ms (profiles/r05/c4_hwq_r05.txt)
+            if not pipelined:
+                s_dig.wait_stream(cur)
+            elif ev_pre[0] is not None:
+                s_dig.wait_event(ev_pre[0])   # no earlier than step i-1's verify kernels (HBM batches
+                #                                would otherwise let the digest streams run steps ahead)
             if from_host:
                 src = uploader.ready_buffer(s_dig)         # uploaded during the previous step
             else:
@@ -901,6 +915,9 @@ def main(argv=None):
             eng.sha512_many_dev(src.data_ptr(), d_boff.data_ptr(), d_blen.data_ptr(), ndig,
                                 d_bouts[di].data_ptr(), s_dig.cuda_stream)
             ev_dig.record(s_dig)
+        if pipelined:
+            ev_pre[0] = torch.cuda.Event()
+            ev_pre[0].record(cur)             # this step's verify kernels start here
         verify_step(cur, o)
         if from_host:
             # host threads stage the NEXT step's batches into pinned memory and DMA them while this
