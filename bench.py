@@ -259,9 +259,17 @@ def cpu_step_with_digests(cb, batches, plan, seconds):
                     "the digests at hash_GBps" % (plan["sigs"], plan["digest_batches"])}
 
 
-def host_fed(eng, cs, slots, zseed, chunks=8, threads=4, reps=5):
-    """C2 through nw_verify_certs from host buffers: ``chunks`` calls over ``threads`` host threads,
-    so one call's host->device copy overlaps another's kernels (each call has its own stream)."""
+def host_fed(eng, cs, slots, zseed, chunks=16, threads=8, reps=5, stream_passes=20):
+    """C2 through nw_verify_certs from pageable host buffers (PCIe and host staging included): what a
+    Rust caller that hands over host buffers sees.  ``chunks`` calls on ``threads`` host threads (every
+    call leases its own workspace and stream, so one call's upload overlaps another's kernels).
+
+    value: STREAMING, the calls of ``stream_passes`` passes submitted back to back on the same threads
+    (a node's Core keeps submitting as batches arrive; no barrier between passes).  passes: the same
+    calls with a barrier after every pass (ms_reps), on reused and on freshly allocated buffers.  About
+    one pass in three to five takes 5-13 ms longer: every calling thread blocks inside hipMemcpyAsync
+    (pinned source) while the GPU idles (HIP API trace, profiles/r05/host_fed_r05.txt); an SDMA-side
+    stall of the runtime (gone with HSA_ENABLE_SDMA=0, whose blit-kernel copies halve the throughput)."""
     from concurrent.futures import ThreadPoolExecutor
     import numpy as np
     bounds = np.linspace(0, cs.ncerts, chunks + 1).astype(int)
@@ -279,8 +287,13 @@ def host_fed(eng, cs, slots, zseed, chunks=8, threads=4, reps=5):
         return [(a, b, c.copy(), d.copy(), e.copy(), f) for a, b, c, d, e, f in ps]
 
     fresh_sets = [fresh(parts) for _ in range(reps)]
+    stream_sets = [fresh(parts) for _ in range(4)]
     with ThreadPoolExecutor(threads) as ex:
         assert all(ex.map(run, parts))   # warm every workspace
+        t0 = time.perf_counter()
+        ok = all(ex.map(run, [p for k in range(stream_passes) for p in stream_sets[k % len(stream_sets)]]))
+        t_stream = time.perf_counter() - t0
+        assert ok
         ts, tf = [], []
         for r in range(reps):
             t0 = time.perf_counter()
@@ -294,12 +307,16 @@ def host_fed(eng, cs, slots, zseed, chunks=8, threads=4, reps=5):
     ts.sort()
     tf.sort()
     dt = ts[len(ts) // 2]
-    return {"value": cs.nsigs / dt, "unit": "sigs/s", "ms": dt * 1e3, "ms_reps": [t * 1e3 for t in ts],
-            "fresh_buffers": {"value": cs.nsigs / tf[len(tf) // 2], "ms": tf[len(tf) // 2] * 1e3,
-                              "ms_reps": [t * 1e3 for t in tf]},
-            "note": "nw_verify_certs on pageable host buffers (every input staged through the call's pinned "
-                    "buffer), %d calls on %d threads, median of %d passes; PCIe and host packing included; "
-                    "fresh_buffers: each pass on newly allocated host arrays" % (chunks, threads, reps)}
+    return {"value": stream_passes * cs.nsigs / t_stream, "unit": "sigs/s",
+            "ms_per_pass_streaming": t_stream / stream_passes * 1e3,
+            "passes": {"value": cs.nsigs / dt, "ms": dt * 1e3, "ms_reps": [t * 1e3 for t in ts],
+                       "fresh_buffers": {"value": cs.nsigs / tf[len(tf) // 2], "ms": tf[len(tf) // 2] * 1e3,
+                                         "ms_reps": [t * 1e3 for t in tf]}},
+            "note": "nw_verify_certs on pageable host buffers (every input staged through the call's pinned buffer), "
+                    "%d calls of ~%d signatures on %d threads; value: %d passes' calls streamed back to back on "
+                    "fresh host arrays (4 rotating sets); passes: a barrier after every pass, median of %d (reused "
+                    "arrays; fresh_buffers: newly allocated ones); PCIe and host packing included"
+                    % (chunks, cs.nsigs // chunks, threads, stream_passes, reps)}
 
 
 class BatchUploader:

@@ -141,6 +141,46 @@ __global__ void __launch_bounds__(64) k_two_lane(uint32_t nb, const uint64_t* kw
     }
 }
 
+// SALU form: the chain's values are wave-uniform (they depend only on kernel
+// arguments), so the compiler keeps them in SGPRs and issues the rounds on the scalar unit: 64-bit
+// s_xor/s_and/s_andn2/s_lshl/s_lshr_b64, s_add_u32 + s_addc_u32, K_t + W_t by s_load.  Plain C
+// operators (no v_bitop3 asm) so nothing forces the values into VGPRs.  One chain per wave, few
+// VGPRs: the question is whether such a chain is fast enough alone (<= 3.4 us per block) to
+// co-issue beside k_verify's VALU waves.
+__device__ __forceinline__ uint64_t srotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+#define NW_RS(a, b, c, d, e, f, g, h, kw)                                                               \
+    do {                                                                                                \
+        const uint64_t t1 = (h) + (kw) + (srotr((e), 14) ^ srotr((e), 18) ^ srotr((e), 41)) +             \
+                            (((e) & (f)) ^ (~(e) & (g)));                                               \
+        const uint64_t t2 = (srotr((a), 28) ^ srotr((a), 34) ^ srotr((a), 39)) +                          \
+                            (((a) & (b)) | ((c) & ((a) | (b))));                                        \
+        (d) += t1;                                                                                      \
+        (h) = t1 + t2;                                                                                  \
+    } while (0)
+__global__ void __launch_bounds__(64) k_rounds_salu(uint32_t nb, const uint64_t* __restrict__ kwin, uint64_t* out,
+                                                    uint64_t* ts) {
+    uint64_t st[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] = SHA512_IV[i];
+    uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    for (uint32_t blk = 0; blk < nb; ++blk) {
+        uint64_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+        for (int q = 0; q < 80; q += 8) {
+            NW_RS(a, b, c, d, e, f, g, h, kwin[q]);      NW_RS(h, a, b, c, d, e, f, g, kwin[q + 1]);
+            NW_RS(g, h, a, b, c, d, e, f, kwin[q + 2]);  NW_RS(f, g, h, a, b, c, d, e, kwin[q + 3]);
+            NW_RS(e, f, g, h, a, b, c, d, kwin[q + 4]);  NW_RS(d, e, f, g, h, a, b, c, kwin[q + 5]);
+            NW_RS(c, d, e, f, g, h, a, b, kwin[q + 6]);  NW_RS(b, c, d, e, f, g, h, a, kwin[q + 7]);
+        }
+        st[0] += a; st[1] += b; st[2] += c; st[3] += d; st[4] += e; st[5] += f; st[6] += g; st[7] += h;
+    }
+    uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < 8; ++i) out[i] = st[i];
+        ts[0] = t1 - t0; ts[1] = r1 - r0;
+    }
+}
+
 // host reference: nb compressions of the fixed (K + W) schedule
 static void host_rounds(uint32_t nb, const uint64_t* kw, uint64_t st[8]) {
     for (int i = 0; i < 8; ++i) st[i] = SHA512_IV[i];
@@ -328,7 +368,8 @@ int main(int argc, char** argv) {
     host_rounds(nb, kw.data(), ref);
     struct V { const char* name; void (*k)(uint32_t, const uint64_t*, uint64_t*, uint64_t*); const uint64_t* in; bool reg_ref; };
     V vs[] = {{"rounds_reg", k_rounds_reg, d_kw, true}, {"rounds_lds", k_rounds_lds, d_kw, true},
-              {"full_inline", k_full_inline, d_blocks, false}, {"two_lane", k_two_lane, d_kwl, true}};
+              {"full_inline", k_full_inline, d_blocks, false}, {"two_lane", k_two_lane, d_kwl, true},
+              {"rounds_salu", k_rounds_salu, d_kw, true}};
     for (const V& v : vs) {
         for (int rep = 0; rep < 3; ++rep) {
             hipLaunchKernelGGL(v.k, dim3(1), dim3(64), 0, 0, nb, v.in, d_out, d_ts);
