@@ -128,36 +128,56 @@ NW_HD void hram_generic(uint32_t out[16], const uint32_t R[8], const uint32_t A[
     sha512_digest_le32(out, st);
 }
 
-// A table entry as gathered: the 30 payload words of its 128-B line (seven 16-B loads and one 8-B
-// load: the two pad words are never fetched into registers).
-struct ent30 {
-    uint4 q[7];
-    uint2 t;
+// A table entry as gathered for a signed digit: (y-x)/2 and (y+x)/2 loaded in the order the sign
+// needs (swapped for a negative digit: -q = ((y-x)/2, (y+x)/2, -d x y)), d x y as stored.  Each half is
+// two 16-B loads and one 8-B load; the two pad words are never fetched into registers.
+struct ent_sw {
+    uint4 m0, m1, p0, p1, c1, c2;
+    uint2 m2, p2, c0;
 };
 
-NW_HD ent30 load_ent30(const uint32_t* __restrict__ p) {
-    ent30 e;
-    const uint4* q = reinterpret_cast<const uint4*>(p);
-#pragma unroll
-    for (int k = 0; k < 7; ++k) e.q[k] = q[k];
-    e.t = reinterpret_cast<const uint2*>(p)[14];
-    return e;
+NW_HD ent_sw load_ent_sw(const uint32_t* __restrict__ e, bool neg) {
+    ent_sw r;
+    const uint32_t* m = e + (neg ? ENT_YPX : ENT_YMX);   // pairs with Y - X
+    const uint32_t* p = e + (neg ? ENT_YMX : ENT_YPX);   // pairs with Y + X
+    r.m0 = reinterpret_cast<const uint4*>(m)[0];
+    r.m1 = reinterpret_cast<const uint4*>(m)[1];
+    r.m2 = reinterpret_cast<const uint2*>(m)[4];
+    r.p0 = reinterpret_cast<const uint4*>(p)[0];
+    r.p1 = reinterpret_cast<const uint4*>(p)[1];
+    r.p2 = reinterpret_cast<const uint2*>(p)[4];
+    r.c0 = reinterpret_cast<const uint2*>(e + ENT_XY2D)[0];
+    r.c1 = reinterpret_cast<const uint4*>(e + ENT_XY2D + 2)[0];
+    r.c2 = reinterpret_cast<const uint4*>(e + ENT_XY2D + 2)[1];
+    return r;
 }
 
-NW_HD ge_precomp ent30_precomp(const ent30& e) {
-    uint32_t w[32];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-        w[4 * k] = e.q[k].x;
-        w[4 * k + 1] = e.q[k].y;
-        w[4 * k + 2] = e.q[k].z;
-        w[4 * k + 3] = e.q[k].w;
-    }
-    w[28] = e.t.x;
-    w[29] = e.t.y;
-    w[30] = 0;
-    w[31] = 0;
-    return ge_precomp_from_words(w);
+NW_HD fe fe_from_q2(const uint4& a, const uint4& b, const uint2& c) {
+    fe f;
+    f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+    f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+    f.v[8] = c.x; f.v[9] = c.y;
+    return f;
+}
+
+// ypx / ymx as loaded (swapped for a negative digit), xy2d as stored (its sign: ge_madd_sgn)
+NW_HD ge_precomp ent_sw_precomp(const ent_sw& e) {
+    ge_precomp q;
+    q.ymx = fe_from_q2(e.m0, e.m1, e.m2);
+    q.ypx = fe_from_q2(e.p0, e.p1, e.p2);
+    fe c;
+    c.v[0] = e.c0.x; c.v[1] = e.c0.y;
+    c.v[2] = e.c1.x; c.v[3] = e.c1.y; c.v[4] = e.c1.z; c.v[5] = e.c1.w;
+    c.v[6] = e.c2.x; c.v[7] = e.c2.y; c.v[8] = e.c2.z; c.v[9] = e.c2.w;
+    q.xy2d = c;
+    return q;
+}
+
+// The chain's first entry: the fully signed entry (d x y negated too) as an extended point.
+NW_HD ge_p3 ent_sw_first(const ent_sw& e, bool neg) {
+    ge_precomp q = ent_sw_precomp(e);
+    q.xy2d = fe_select_mask(q.xy2d, fe_neg(q.xy2d), lane_mask(neg));
+    return ge_from_precomp(q);
 }
 
 // One comb pass: P += sum_pos sign(d_pos) * T[pos][|d_pos|] for the signed radix-2^W digits of
@@ -173,34 +193,33 @@ template <int W, bool FIRST, bool FUSED = false>
 NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab, bool neg_pos) {
     int carry = 0;
     int d = next_digit<W>(sc, carry);
-    ent30 cur = load_ent30(tab + (size_t)(d < 0 ? -d : d) * PRECOMP_WORDS);
+    bool ng = neg_pos ? d > 0 : d < 0;
+    ent_sw cur = load_ent_sw(tab + (size_t)(d < 0 ? -d : d) * PRECOMP_WORDS, ng);
     int pos = 0;
     if constexpr (FIRST) {
         // position 0 starts the chain: P = T[0][|d|] (sign applied), no addition
-        const ge_precomp q0 = ent30_precomp(cur);
-        const bool neg0 = neg_pos ? d > 0 : d < 0;
+        const ent_sw e0 = cur;
+        const bool neg0 = ng;
         d = next_digit<W>(sc, carry);   // position 1's digit; its gather overlaps the conversion
-        cur = load_ent30(tab + ((size_t)comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
-        P = ge_from_precomp(ge_precomp_cneg(q0, neg0));
+        ng = neg_pos ? d > 0 : d < 0;
+        cur = load_ent_sw(tab + ((size_t)comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS, ng);
+        P = ent_sw_first(e0, neg0);
         pos = 1;
     }
 #pragma nounroll
     for (; pos < comb_pos(W); ++pos) {
         int dn = 0;
-#ifdef NW_NO_PREFETCH
-        cur = load_ent30(tab + ((size_t)pos * comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
-        if (pos + 1 < comb_pos(W)) dn = next_digit<W>(sc, carry);
-        P = ge_madd<FUSED>(P, ge_precomp_cneg(ent30_precomp(cur), neg_pos ? d > 0 : d < 0));
-#else
-        ent30 nxt;
+        bool ngn = false;
+        ent_sw nxt;
         if (pos + 1 < comb_pos(W)) {
             dn = next_digit<W>(sc, carry);
-            nxt = load_ent30(tab + ((size_t)(pos + 1) * comb_ent(W) + (dn < 0 ? -dn : dn)) * PRECOMP_WORDS);
+            ngn = neg_pos ? dn > 0 : dn < 0;
+            nxt = load_ent_sw(tab + ((size_t)(pos + 1) * comb_ent(W) + (dn < 0 ? -dn : dn)) * PRECOMP_WORDS, ngn);
         }
-        P = ge_madd<FUSED>(P, ge_precomp_cneg(ent30_precomp(cur), neg_pos ? d > 0 : d < 0));
+        P = ge_madd_sgn<FUSED>(P, ent_sw_precomp(cur), lane_mask(ng));
         cur = nxt;
-#endif
         d = dn;
+        ng = ngn;
     }
 }
 
@@ -210,27 +229,32 @@ template <int W, bool FIRST, bool FUSED>
 __device__ __forceinline__ void comb_pass_dig(ge_p3& P, const int* dig, int stride, const uint32_t* __restrict__ tab,
                                               bool neg_pos) {
     int d = dig[0];
-    ent30 cur = load_ent30(tab + (size_t)(d < 0 ? -d : d) * PRECOMP_WORDS);
+    bool ng = neg_pos ? d > 0 : d < 0;
+    ent_sw cur = load_ent_sw(tab + (size_t)(d < 0 ? -d : d) * PRECOMP_WORDS, ng);
     int pos = 0;
     if constexpr (FIRST) {
-        const ge_precomp q0 = ent30_precomp(cur);
-        const bool neg0 = neg_pos ? d > 0 : d < 0;
+        const ent_sw e0 = cur;
+        const bool neg0 = ng;
         d = dig[stride];
-        cur = load_ent30(tab + ((size_t)comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS);
-        P = ge_from_precomp(ge_precomp_cneg(q0, neg0));
+        ng = neg_pos ? d > 0 : d < 0;
+        cur = load_ent_sw(tab + ((size_t)comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS, ng);
+        P = ent_sw_first(e0, neg0);
         pos = 1;
     }
 #pragma nounroll
     for (; pos < comb_pos(W); ++pos) {
         int dn = 0;
-        ent30 nxt;
+        bool ngn = false;
+        ent_sw nxt;
         if (pos + 1 < comb_pos(W)) {
             dn = dig[(pos + 1) * stride];
-            nxt = load_ent30(tab + ((size_t)(pos + 1) * comb_ent(W) + (dn < 0 ? -dn : dn)) * PRECOMP_WORDS);
+            ngn = neg_pos ? dn > 0 : dn < 0;
+            nxt = load_ent_sw(tab + ((size_t)(pos + 1) * comb_ent(W) + (dn < 0 ? -dn : dn)) * PRECOMP_WORDS, ngn);
         }
-        P = ge_madd<FUSED>(P, ge_precomp_cneg(ent30_precomp(cur), neg_pos ? d > 0 : d < 0));
+        P = ge_madd_sgn<FUSED>(P, ent_sw_precomp(cur), lane_mask(ng));
         cur = nxt;
         d = dn;
+        ng = ngn;
     }
 }
 
@@ -423,14 +447,10 @@ NW_HD void comb_entry_one(const uint32_t* bases, uint32_t pos, uint32_t e, uint3
         q = ge_to_precomp(acc);
     }
     uint32_t* dst = tab + ((size_t)pos * comb_ent(W) + e) * PRECOMP_WORDS;
+    uint32_t w[32];
+    precomp_to_words(q, w);
 #pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        dst[k] = q.ypx.v[k];
-        dst[10 + k] = q.ymx.v[k];
-        dst[20 + k] = q.xy2d.v[k];
-    }
-    dst[30] = 0;
-    dst[31] = 0;
+    for (int k = 0; k < 32; ++k) dst[k] = w[k];
 }
 
 // Comb-table builder for entries [CH c, CH c + CH) of one (key, position): consecutive multiples
@@ -486,11 +506,10 @@ NW_HD void comb_chunk_build(const uint32_t* bases, uint32_t pos, uint32_t c, uin
             const fe x = fe_mul(load_fe(sl), zi);
             const fe y = fe_mul(load_fe(sl + 10), zi);
             const ge_precomp q = ge_precomp_from_affine(x, y);
-            store_fe(sl, q.ypx);
-            store_fe(sl + 10, q.ymx);
-            store_fe(sl + 20, q.xy2d);
-            sl[30] = 0;
-            sl[31] = 0;
+            uint32_t w[32];
+            precomp_to_words(q, w);
+#pragma unroll
+            for (int j = 0; j < 32; ++j) sl[j] = w[j];
         }
     }
 }

@@ -78,14 +78,7 @@ NW_HD void store_niels_affine(uint32_t* dst, const ge_p3& p) {
     const ge_precomp e = ge_precomp_from_affine(p.X, p.Y);
     uint4* q = reinterpret_cast<uint4*>(dst);
     uint32_t w[32];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) {
-        w[k] = e.ypx.v[k];
-        w[10 + k] = e.ymx.v[k];
-        w[20 + k] = e.xy2d.v[k];
-    }
-    w[30] = 0;
-    w[31] = 0;
+    precomp_to_words(e, w);
 #pragma unroll
     for (int k = 0; k < 8; ++k) q[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
@@ -420,29 +413,18 @@ __global__ void __launch_bounds__(64 * MSM_BUCKET_WAVES) k_msm_bucket(MsmParams 
         uint32_t cb = idx[p0] >> 16;
         bool head = p0 > 0 && (idx[p0 - 1] >> 16) == cb;
         uint32_t v = idx[p0];
-        const uint4* qn = reinterpret_cast<const uint4*>(ent + (size_t)(v & 0x7FFFu) * MSM_ENT_WORDS);
-        uint4 nx[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) nx[k] = qn[k];
+        // the entry's halves are loaded in the order the digit's sign needs (load_ent_sw): no
+        // select between the gather and the products
+        ent_sw nx = load_ent_sw(ent + (size_t)(v & 0x7FFFu) * MSM_ENT_WORDS, (v & 0x8000u) != 0);
 #pragma nounroll
         for (uint32_t p = p0; p < p1; ++p) {
-            uint32_t w[32];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                w[4 * k] = nx[k].x;
-                w[4 * k + 1] = nx[k].y;
-                w[4 * k + 2] = nx[k].z;
-                w[4 * k + 3] = nx[k].w;
-            }
+            const ent_sw cur = nx;
             const bool neg = (v & 0x8000u) != 0;
             const uint32_t vn = p + 1 < p1 ? idx[p + 1] : v;
-            if (p + 1 < p1) {   // prefetch the next entry under this addition
-                const uint4* q2 = reinterpret_cast<const uint4*>(ent + (size_t)(vn & 0x7FFFu) * MSM_ENT_WORDS);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) nx[k] = q2[k];
-            }
+            if (p + 1 < p1)   // prefetch the next entry under this addition
+                nx = load_ent_sw(ent + (size_t)(vn & 0x7FFFu) * MSM_ENT_WORDS, (vn & 0x8000u) != 0);
             // fused-carry product groups: two waves share each SIMD here (412 vs 424 us per launch)
-            acc = ge_madd<true>(acc, ge_precomp_cneg(ge_precomp_from_words(w), neg));
+            acc = ge_madd_sgn<true>(acc, ent_sw_precomp(cur), lane_mask(neg));
             const bool last = p + 1 == p1;
             const bool brk = last || (vn >> 16) != cb;   // the run of bucket cb ends here
             if (brk) {

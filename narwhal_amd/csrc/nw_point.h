@@ -25,7 +25,13 @@ struct ge_cached {
 };
 
 // Table entry layout in HBM: 32 u32 words = 128 B (one cache line):
-//   [0..9] (y+x)/2, [10..19] (y-x)/2, [20..29] d x y, [30..31] zero pad.
+//   [0..9] (y+x)/2, [10..11] zero, [12..21] (y-x)/2, [22..31] d x y.
+// (y+x)/2 and (y-x)/2 both start 16-byte aligned, so a comb step loads them in either order by
+// address: the conditional negation of a signed digit (-q swaps the two and negates d x y) costs no
+// select between the gather and the first products (comb_pass_dig; the sign of d x y is applied
+// to the product T d x y instead, ge_madd_sgn).  Round 4's layout ([0..9] [10..19] [20..29], pad)
+// needed the entry whole before 30 selects: k_verify 1.12 ms at C2 against 0.95 without them.
+static constexpr int ENT_YPX = 0, ENT_YMX = 12, ENT_XY2D = 22;
 #ifndef NW_HALF_NIELS
 #define NW_HALF_NIELS 1
 #endif
@@ -134,6 +140,44 @@ NW_HD ge_p3 ge_madd_s2(const madd_mid& m) {
 
 template <bool FUSED = false>
 NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) { return ge_madd_s2<FUSED>(ge_madd_s1<FUSED>(p, q)); }
+
+// p + (q or -q) for an entry whose (y+x)/2 and (y-x)/2 were already swapped when negated (loaded in
+// that order, load_ent_sw) and whose d x y was NOT: the sign lands on the product c = T d x y
+// instead.  -q's f and g are q's g and f (F/2 = Z - C/2, G/2 = Z + C/2 with C negated), so with the
+// mask m all-ones f = Z + c and g = Z + 2p - c (k = 3: g feeds fe_mul4_efgh as a first operand
+// against h, k = 2, and f, k <= 3: products 6 and 9 <= 32).
+template <bool FUSED>
+NW_HD madd_mid ge_madd_s1_sgn(const ge_p3& p, const ge_precomp& q, uint32_t m) {
+    madd_mid r;
+    fe a, b, c;
+    if constexpr (FUSED && NW_MADD3) {
+        fe_mul3(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx, c, p.T, q.xy2d);
+    } else if constexpr (FUSED) {
+        fe_mul2(a, fe_sub_loose(p.Y, p.X), q.ymx, b, fe_add(p.Y, p.X), q.ypx);
+        c = fe_mul(p.T, q.xy2d);
+    } else {
+        a = fe_mul(fe_sub_loose(p.Y, p.X), q.ymx);
+        b = fe_mul(fe_add(p.Y, p.X), q.ypx);
+        c = fe_mul(p.T, q.xy2d);
+    }
+    r.e = fe_sub_loose(b, a);
+    r.h = fe_add(b, a);
+    const fe fq = fe_sub2p_loose(p.Z, c), gq = fe_add(p.Z, c);
+#ifdef NW_TIMING_NO_FG_SELECT   // timing-only variant builds (wrong verdicts)
+    (void)m;
+    r.f = fq;
+    r.g = gq;
+#else
+    r.f = fe_select_mask(fq, gq, m);
+    r.g = fe_select_mask(gq, fq, m);
+#endif
+    return r;
+}
+
+template <bool FUSED = false>
+NW_HD ge_p3 ge_madd_sgn(const ge_p3& p, const ge_precomp& q, uint32_t m) {
+    return ge_madd_s2<FUSED>(ge_madd_s1_sgn<FUSED>(p, q, m));
+}
 
 // Extended point of a halved affine Niels entry, with no field multiplication beyond T:
 // X = (y+x)/2 - (y-x)/2 = x, Y = y, Z = 1, T = xy = (d x y) / d.
@@ -323,6 +367,9 @@ NW_HD bool y_is_small_order(const uint32_t yw[8]) {
 
 // Conditionally negate an affine Niels entry: -(x, y) = (-x, y) swaps y+x / y-x and negates 2dxy.
 NW_HD ge_precomp ge_precomp_cneg(const ge_precomp& q, bool neg) {
+#ifdef NW_TIMING_NO_CNEG   // timing-only variant builds (wrong verdicts): the cost of the negation
+    return q;
+#endif
     ge_precomp r = q;
     const uint32_t m = lane_mask(neg);
     fe_cswap_mask(r.ypx, r.ymx, m);
@@ -334,11 +381,23 @@ NW_HD ge_precomp ge_precomp_from_words(const uint32_t* w) {
     ge_precomp q;
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
-        q.ypx.v[i] = w[i];
-        q.ymx.v[i] = w[10 + i];
-        q.xy2d.v[i] = w[20 + i];
+        q.ypx.v[i] = w[ENT_YPX + i];
+        q.ymx.v[i] = w[ENT_YMX + i];
+        q.xy2d.v[i] = w[ENT_XY2D + i];
     }
     return q;
+}
+
+// The 32 words of a table entry (the layout above).
+NW_HD void precomp_to_words(const ge_precomp& q, uint32_t* w) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+        w[ENT_YPX + i] = q.ypx.v[i];
+        w[ENT_YMX + i] = q.ymx.v[i];
+        w[ENT_XY2D + i] = q.xy2d.v[i];
+    }
+    w[10] = 0;
+    w[11] = 0;
 }
 
 // Table-entry (halved affine Niels) form of p (one inversion); tight limbs.

@@ -102,42 +102,28 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
         if (base) shift_window<WB>(sp);
         else shift_window<WA>(hp);
     }
-    auto entry = [&](int st) -> const uint4* {
+    auto negs = [&](int st) -> bool {
+        const int pos = p0 + st;
+        return pos < NPOS && (pos < PB ? dig[st] < 0 : dig[st] > 0);
+    };
+    // entries loaded in the order their digit's sign needs (load_ent_sw)
+    auto entry = [&](int st) -> ent_sw {
         const int pos = p0 + st;
         const uint32_t ad = (uint32_t)(dig[st] < 0 ? -dig[st] : dig[st]);
         // past the last position: entry 0 of base position 0 (the identity), a no-op addition
         const uint32_t* e = pos >= NPOS ? a.btab
                             : pos < PB  ? a.btab + ((size_t)pos * comb_ent(WB) + ad) * PRECOMP_WORDS
                                         : atab + ((size_t)(pos - PB) * comb_ent(WA) + ad) * PRECOMP_WORDS;
-        return reinterpret_cast<const uint4*>(e);
+        return load_ent_sw(e, negs(st));
     };
-    uint4 nx[8];
-    {
-        const uint4* q = entry(0);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) nx[k] = q[k];
-    }
+    ent_sw nx = entry(0);
     ge_p3 P;
 #pragma unroll
     for (int st = 0; st < K; ++st) {
-        const int pos = p0 + st;
-        uint32_t w[32];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            w[4 * k] = nx[k].x;
-            w[4 * k + 1] = nx[k].y;
-            w[4 * k + 2] = nx[k].z;
-            w[4 * k + 3] = nx[k].w;
-        }
-        if (st + 1 < K) {
-            const uint4* q = entry(st + 1);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) nx[k] = q[k];
-        }
-        const bool neg = pos < NPOS && (pos < PB ? dig[st] < 0 : dig[st] > 0);
-        const ge_precomp ent = ge_precomp_cneg(ge_precomp_from_words(w), neg);
-        if (st == 0) P = ge_from_precomp(ent);
-        else P = ge_madd(P, ent);
+        const ent_sw cur = nx;
+        if (st + 1 < K) nx = entry(st + 1);
+        if (st == 0) P = ent_sw_first(cur, negs(st));
+        else P = ge_madd_sgn(P, ent_sw_precomp(cur), lane_mask(negs(st)));
     }
 #pragma unroll
     for (int off = 1; off < VERIFY_SPLIT; off <<= 1) {
