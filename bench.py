@@ -1094,7 +1094,7 @@ def main(argv=None):
             "data": "synthetic (GPU-signed RFC 8032 signatures over SHA-512 certificate digests)",
             "config": {"workload": workload_desc, "baseline_config": plan["baseline"],
                        "validators": plan["validators"], "certs_per_gpu": cs.ncerts, "votes_per_cert": plan["votes"],
-                       "key_window": kw,
+                       "key_window": kw, "key_negtab": eng.key_negtab(),
                        "parallelism": "certificate shards per GPU; RCCL all_gather of verdict bitmaps + stake"},
             "p50_cert_latency_ms": lat[len(lat) // 2] * 1e3 if lat else None,
             "p99_cert_latency_ms": lat[int(len(lat) * 0.99)] * 1e3 if lat else None,

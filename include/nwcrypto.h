@@ -115,6 +115,10 @@ size_t nw_committee_size(const nw_ctx* ctx);
 /* Key comb window in use (8 / 12 / 16 / 20; 0 before the first load, or -1 while committee mode
  * has not sized it yet). */
 int nw_key_window(const nw_ctx* ctx);
+/* 1 when every cached key table is stored with its negated copy (decided at the first load: when
+ * twice the tables fit the HBM budget; NWCRYPTO_KEY_NEGTAB=0 disables), else 0.  Verdicts are the
+ * same either way; only k_verify's key pass differs (no conditional negation with the copies). */
+int nw_key_negtab(const nw_ctx* ctx);
 /* Basepoint comb window this library was built with (additions per s*B = ceil(256 / w)). */
 int nw_base_window(void);
 

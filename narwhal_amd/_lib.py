@@ -76,6 +76,7 @@ def _load() -> ctypes.CDLL:
         "nw_committee_load": (I, [P, P, P, S, P]),
         "nw_committee_size": (S, [P]),
         "nw_key_window": (I, [P]),
+        "nw_key_negtab": (I, [P]),
         "nw_base_window": (I, []),
         "nw_verify_strict": (I, [P, P, S, P, P]),
         "nw_verify_strict_many": (I, [P, P, P, P, P, S, P]),
@@ -181,6 +182,9 @@ class Engine:
 
     def key_window(self) -> int:
         return LIB.nw_key_window(self._ctx)
+
+    def key_negtab(self) -> bool:
+        return bool(LIB.nw_key_negtab(self._ctx))
 
     @staticmethod
     def base_window() -> int:

@@ -177,7 +177,8 @@ struct nw_ctx {
     bool committee_mode = false;  // nw_opts.key_window == -1
     bool key_reserve = false;     // committee mode + max_keys: the first load allocates max_keys slots
     bool budget_fixed = false;    // window, max_keys and reservation decided (first load with keys)
-    size_t key_words = 0;         // u32 words per key table
+    size_t key_words = 0;         // u32 words per key-cache slot (T+, and T- when key_negtab)
+    bool key_negtab = false;      // each key table followed by its negated copy (k_verify: no negation)
     size_t nkeys = 0, key_cap = 0;
     uint32_t* d_keys_raw = nullptr;
     uint32_t* d_key_info = nullptr;
@@ -406,11 +407,23 @@ int committee_window(size_t n, double headroom, size_t budget) {
 
 void fix_window(nw_ctx* ctx, size_t first_load) {
     const size_t budget = key_budget(ctx);
+    const bool auto_window = ctx->key_window == 0;
     if (ctx->key_window == -1)
         ctx->key_window = ctx->max_keys_user ? committee_window(std::max(ctx->max_keys, first_load), 1.0, budget)
                                              : committee_window(first_load, 1.25, budget);
     if (ctx->key_window == 0) ctx->key_window = first_load <= 384 ? 16 : (first_load <= 12288 ? 12 : 8);
-    ctx->key_words = comb_words(ctx->key_window);
+    // Negated copies (T-) of the key tables when twice the tables still fit the budget for the keys
+    // this context is sized for: k_verify's key pass then needs no conditional negation (7% of its
+    // time at C2).  A large worker cache keeps the wider window instead (2 fewer comb positions are
+    // worth more than the negation).  NWCRYPTO_KEY_NEGTAB=0 turns it off (A/B).
+    // (sized for: the declared max_keys, else the first load with committee mode's 25% headroom; an
+    // automatic window leaves room for 4x the first load)
+    const double sized = ctx->max_keys_user ? (double)std::max(ctx->max_keys, first_load)
+                                            : (double)first_load * (auto_window ? 4.0 : 1.25);
+    const char* env = getenv("NWCRYPTO_KEY_NEGTAB");
+    ctx->key_negtab = !(env && env[0] == '0') &&
+                      2.0 * sized * (double)comb_words(ctx->key_window) * 4.0 <= (double)budget;
+    ctx->key_words = comb_words(ctx->key_window) * (ctx->key_negtab ? 2 : 1);
     ctx->key_reserve = ctx->max_keys_user && ctx->committee_mode;
     ctx->budget_fixed = true;
     if (!ctx->max_keys_user) ctx->max_keys = budget / (ctx->key_words * 4);
@@ -464,16 +477,16 @@ int grow_keys(nw_ctx* ctx, size_t need) {
 }
 
 // Build tables for nk keys whose raw bytes are already at d_raw (administrative stream).
-int build_keys(nw_ctx* ctx, uint32_t* d_raw, uint32_t* d_info, uint32_t* d_tab, size_t nk, int window) {
+int build_keys(nw_ctx* ctx, uint32_t* d_raw, uint32_t* d_info, uint32_t* d_tab, size_t nk, int window, size_t stride,
+               bool negtab) {
     // keys per launch: bounds the bases scratch and keeps a launch near 16M chunk threads
     const size_t chunk = window >= 24 ? 1 : (window == 20 ? 16 : (window == 16 ? 256 : 4096));
-    const size_t words = comb_words(window);
     for (size_t s = 0; s < nk; s += chunk) {
         const size_t m = nk - s < chunk ? nk - s : chunk;
         if (m * comb_pos(window) * 40 * 4 > ctx->w_bases.cap) NW_TRY(hipStreamSynchronize(ctx->stream), "sync");
         NW_TRY(ctx->w_bases.ensure(m * comb_pos(window) * 40 * 4), "hipMalloc(bases)");
-        NW_TRY(launch_key_prep((uint32_t)m, d_raw + s * 8, d_info + s, ctx->w_bases.as<uint32_t>(), d_tab + s * words,
-                               window, ctx->stream),
+        NW_TRY(launch_key_prep((uint32_t)m, d_raw + s * 8, d_info + s, ctx->w_bases.as<uint32_t>(), d_tab + s * stride,
+                               stride, negtab, window, ctx->stream),
                "k_key_prep/k_comb_build");
     }
     return NW_OK;
@@ -528,7 +541,7 @@ int ensure_slots(nw_ctx* ctx, const uint8_t (*pk)[32], const uint32_t* stake, si
         NW_TRY(hipMemcpyAsync(ctx->d_keys_raw + k0 * 8, new_raw.data(), add * 32, hipMemcpyHostToDevice, ctx->stream),
                "H2D keys");
         rc = build_keys(ctx, ctx->d_keys_raw + k0 * 8, ctx->d_key_info + k0, ctx->d_key_tab + k0 * ctx->key_words,
-                        add, ctx->key_window);
+                        add, ctx->key_window, ctx->key_words, ctx->key_negtab);
         if (rc != NW_OK) {
             (void)hipStreamSynchronize(ctx->stream);
             return rc;
@@ -674,6 +687,8 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     vp.keys_raw = ctx->d_keys_raw;
     vp.key_info = ctx->d_key_info;
     vp.key_tab = ctx->d_key_tab;
+    vp.key_stride = ctx->key_words;
+    vp.key_negtab = ctx->key_negtab ? 1u : 0u;
     vp.nkeys = (uint32_t)ctx->nkeys;
     vp.btab = ctx->d_btab;
     static const uint8_t kNoSeed[32] = {0};   // strict-only calls draw no coefficients
@@ -1173,6 +1188,66 @@ const char* nw_version(void) { return "nwcrypto 0.3 gfx950 " __DATE__; }
 
 int nw_abi_version(void) { return NW_ABI_VERSION; }
 
+namespace {
+// The basepoint comb (one "key" = B; with its negated copy when B_NEGTAB) is shared by every context
+// of the process on a device, reference-counted: a node running its primary's and its workers'
+// engines in one process holds one copy (11.8 GB per table at W24, 42.9 GB at W26).  The registry is
+// never destroyed (contexts may be released during interpreter shutdown).
+struct BaseTable {
+    uint32_t* p = nullptr;
+    int refs = 0;
+};
+std::mutex& base_mu() {
+    static std::mutex* m = new std::mutex();
+    return *m;
+}
+std::unordered_map<int, BaseTable>& base_tables() {
+    static auto* t = new std::unordered_map<int, BaseTable>();
+    return *t;
+}
+
+int acquire_base(nw_ctx* ctx) {
+    std::lock_guard<std::mutex> g(base_mu());
+    BaseTable& b = base_tables()[ctx->device];
+    if (!b.p) {
+        uint32_t* tab = nullptr;
+        uint32_t* d_braw = nullptr;
+        uint32_t* d_binfo = nullptr;
+        int rc = NW_OK;
+        if (hipMalloc(&tab, B_TABLES * comb_words(B_WINDOW) * 4) != hipSuccess || hipMalloc(&d_braw, 32) != hipSuccess ||
+            hipMalloc(&d_binfo, 16) != hipSuccess)
+            rc = NW_ERR_NOMEM;
+        if (rc == NW_OK && hipMemcpy(d_braw, kBaseEnc, 32, hipMemcpyHostToDevice) != hipSuccess) rc = NW_ERR_DEVICE;
+        if (rc == NW_OK)
+            rc = build_keys(ctx, d_braw, d_binfo, tab, 1, B_WINDOW, B_TABLES * comb_words(B_WINDOW), B_NEGTAB);
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == NW_OK) rc = NW_ERR_DEVICE;
+        ctx->w_bases.release();   // the basepoint's bases scratch is not the committee's
+        for (uint32_t* q : {d_braw, d_binfo})
+            if (q) (void)hipFree(q);
+        if (rc != NW_OK) {
+            if (tab) (void)hipFree(tab);
+            return rc;
+        }
+        b.p = tab;
+    }
+    ++b.refs;
+    ctx->d_btab = b.p;
+    return NW_OK;
+}
+
+void release_base(nw_ctx* ctx) {
+    if (!ctx->d_btab) return;
+    std::lock_guard<std::mutex> g(base_mu());
+    BaseTable& b = base_tables()[ctx->device];
+    if (--b.refs == 0) {
+        (void)hipDeviceSynchronize();   // no other context's work may still read it (none holds it)
+        (void)hipFree(b.p);
+        b.p = nullptr;
+    }
+    ctx->d_btab = nullptr;
+}
+}  // namespace
+
 int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     if (!out) return NW_ERR_ARG;
     *out = nullptr;
@@ -1195,27 +1270,12 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     if (opts && opts->key_window) {
         ctx->key_window = opts->key_window;
         ctx->committee_mode = ctx->key_window == -1;
-        if (ctx->key_window > 0) ctx->key_words = comb_words(ctx->key_window);   // budget: at the first load
     }
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
         delete ctx;
         return NW_ERR_DEVICE;
     }
-    // basepoint comb (one "key" = B)
-    uint32_t* d_braw = nullptr;
-    uint32_t* d_binfo = nullptr;
-    if (hipMalloc(&ctx->d_btab, comb_words(B_WINDOW) * 4) != hipSuccess || hipMalloc(&d_braw, 32) != hipSuccess ||
-        hipMalloc(&d_binfo, 16) != hipSuccess) {
-        if (d_braw) (void)hipFree(d_braw);
-        nw_ctx_destroy(ctx);
-        return NW_ERR_NOMEM;
-    }
-    int rc = NW_OK;
-    if (hipMemcpy(d_braw, kBaseEnc, 32, hipMemcpyHostToDevice) != hipSuccess) rc = NW_ERR_DEVICE;
-    if (rc == NW_OK) rc = build_keys(ctx, d_braw, d_binfo, ctx->d_btab, 1, B_WINDOW);
-    if (hipStreamSynchronize(ctx->stream) != hipSuccess && rc == NW_OK) rc = NW_ERR_DEVICE;
-    (void)hipFree(d_braw);
-    (void)hipFree(d_binfo);
+    const int rc = acquire_base(ctx);
     if (rc != NW_OK) {
         nw_ctx_destroy(ctx);
         return rc;
@@ -1240,8 +1300,9 @@ void nw_ctx_destroy(nw_ctx* ctx) {
         (void)hipEventDestroy(ev.first);
         (void)hipEventDestroy(ev.second);
     }
-    for (uint32_t* p : {ctx->d_btab, ctx->d_keys_raw, ctx->d_key_info, ctx->d_stake, ctx->d_key_tab})
+    for (uint32_t* p : {ctx->d_keys_raw, ctx->d_key_info, ctx->d_stake, ctx->d_key_tab})
         if (p) (void)hipFree(p);
+    release_base(ctx);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1291,6 +1352,12 @@ int nw_key_window(const nw_ctx* ctx) {
     if (!ctx) return 0;
     std::shared_lock<std::shared_mutex> g(const_cast<nw_ctx*>(ctx)->keys_mu);
     return ctx->key_window;
+}
+
+int nw_key_negtab(const nw_ctx* ctx) {
+    if (!ctx) return 0;
+    std::shared_lock<std::shared_mutex> g(const_cast<nw_ctx*>(ctx)->keys_mu);
+    return ctx->key_negtab ? 1 : 0;
 }
 
 int nw_base_window(void) { return B_WINDOW; }

@@ -225,36 +225,64 @@ NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab,
 
 // comb_pass with the signed digits precomputed (dig[pos * stride], the lane's slot of a shared
 // array): the 8-word scalar and its carry are not live during the additions (k_verify, NW_DIG_LDS).
-template <int W, bool FIRST, bool FUSED>
+// NT: the table is followed by its negated copy T- (tab + comb_words(W), k_comb_negate): a digit's
+// sign only picks the address, and the addition is the plain ge_madd (no swap, no f/g selects).
+// LAST: the chain's final addition computes X, Y, Z only (ge_madd_s2_xyz; P.T is left zero).
+template <int W, bool FIRST, bool FUSED, bool NT = false, bool LAST = false>
 __device__ __forceinline__ void comb_pass_dig(ge_p3& P, const int* dig, int stride, const uint32_t* __restrict__ tab,
                                               bool neg_pos) {
+    auto gather = [&](int pos, int d, bool ng) -> ent_sw {
+#ifdef NW_TIMING_HOT_ENTRIES   // timing-only variant builds (wrong verdicts): 16 L2-resident entries per position
+        const uint32_t* e = tab + ((size_t)pos * comb_ent(W) + ((d < 0 ? -d : d) & 15)) * PRECOMP_WORDS;
+#else
+        const uint32_t* e = tab + ((size_t)pos * comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS;
+#endif
+#ifdef NW_TIMING_HALF_LINE   // timing-only: every load from the entry's first 64 B (same VALU, half the bytes)
+        ent_sw r = load_ent_sw(e + (NT && ng ? comb_words(W) : 0), false);
+        const uint4* h = reinterpret_cast<const uint4*>(e + (NT && ng ? comb_words(W) : 0));
+        r.p0 = h[2]; r.p1 = h[3]; r.c1 = h[0]; r.c2 = h[1];
+        r.p2 = reinterpret_cast<const uint2*>(h)[2]; r.c0 = reinterpret_cast<const uint2*>(h)[3];
+        return r;
+#endif
+        if constexpr (NT) return load_ent_sw(e + (ng ? comb_words(W) : 0), false);
+        else return load_ent_sw(e, ng);
+    };
     int d = dig[0];
     bool ng = neg_pos ? d > 0 : d < 0;
-    ent_sw cur = load_ent_sw(tab + (size_t)(d < 0 ? -d : d) * PRECOMP_WORDS, ng);
+    ent_sw cur = gather(0, d, ng);
     int pos = 0;
     if constexpr (FIRST) {
         const ent_sw e0 = cur;
         const bool neg0 = ng;
         d = dig[stride];
         ng = neg_pos ? d > 0 : d < 0;
-        cur = load_ent_sw(tab + ((size_t)comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS, ng);
-        P = ent_sw_first(e0, neg0);
+        cur = gather(1, d, ng);
+        if constexpr (NT) P = ge_from_precomp(ent_sw_precomp(e0));
+        else P = ent_sw_first(e0, neg0);
         pos = 1;
     }
 #pragma nounroll
-    for (; pos < comb_pos(W); ++pos) {
+    for (; pos < comb_pos(W) - (LAST ? 1 : 0); ++pos) {
         int dn = 0;
         bool ngn = false;
         ent_sw nxt;
         if (pos + 1 < comb_pos(W)) {
             dn = dig[(pos + 1) * stride];
             ngn = neg_pos ? dn > 0 : dn < 0;
-            nxt = load_ent_sw(tab + ((size_t)(pos + 1) * comb_ent(W) + (dn < 0 ? -dn : dn)) * PRECOMP_WORDS, ngn);
+            nxt = gather(pos + 1, dn, ngn);
         }
-        P = ge_madd_sgn<FUSED>(P, ent_sw_precomp(cur), lane_mask(ng));
+        if constexpr (NT) P = ge_madd<FUSED>(P, ent_sw_precomp(cur));
+        else P = ge_madd_sgn<FUSED>(P, ent_sw_precomp(cur), lane_mask(ng));
+#ifdef NW_TIMING_EXTRA_SQ   // timing-only: one more squaring per step (+55 MADs), folded into T
+        P.T = fe_add(P.T, fe_sq(P.Z));
+#endif
         cur = nxt;
         d = dn;
         ng = ngn;
+    }
+    if constexpr (LAST) {
+        if constexpr (NT) P = ge_madd_s2_xyz<FUSED>(ge_madd_s1<FUSED>(P, ent_sw_precomp(cur)));
+        else P = ge_madd_s2_xyz<FUSED>(ge_madd_s1_sgn<FUSED>(P, ent_sw_precomp(cur), lane_mask(ng)));
     }
 }
 
@@ -359,15 +387,19 @@ NW_HD uint32_t verify_pflags(const ge_p3& P, const uint32_t R[8], uint32_t parti
 // the sign bit is set, and accepts x = 0 with the sign bit set).
 //   MATCH  <=> R decodes (dalek decompress) and decode(R) == P  (the strict equation R = sB - hA)
 //   STRICT <=> verify_strict accepts (adds: S ok, A ok, neither R nor A of small order)
-NW_HD uint32_t finish_x_flags(const fe& X, const fe& zi, uint32_t pf) {
-    uint32_t xw[8];
-    fe_tobytes_w(xw, fe_mul(X, zi));
-    const bool x_zero = (xw[0] | xw[1] | xw[2] | xw[3] | xw[4] | xw[5] | xw[6] | xw[7]) == 0;
-    const bool match = (pf & PF_YMATCH) && (x_zero || ((xw[0] & 1u) == ((pf & PF_RSIGN) ? 1u : 0u)));
+NW_HD uint32_t finish_flags(uint32_t pf, bool xmatch) {
+    const bool match = (pf & PF_YMATCH) && xmatch;
     const bool sok = (pf & NW_F_S_OK) != 0, aok = (pf & NW_F_A_OK) != 0;
     const bool asmall = (pf & NW_F_A_SMALL) != 0, rsmall = (pf & NW_F_R_SMALL) != 0;
     const bool strict = sok && aok && match && !asmall && !rsmall;
     return (pf & ~PF_INTERNAL) | (match ? NW_F_MATCH : 0u) | (strict ? NW_F_STRICT : 0u);
+}
+
+NW_HD uint32_t finish_x_flags(const fe& X, const fe& zi, uint32_t pf) {
+    uint32_t xw[8];
+    fe_tobytes_w(xw, fe_mul(X, zi));
+    const bool x_zero = (xw[0] | xw[1] | xw[2] | xw[3] | xw[4] | xw[5] | xw[6] | xw[7]) == 0;
+    return finish_flags(pf, x_zero || ((xw[0] & 1u) == ((pf & PF_RSIGN) ? 1u : 0u)));
 }
 
 // Flags from P (with zi = 1/Z_P) against the signature's R encoding (both halves).

@@ -58,8 +58,10 @@ struct VerifyParams {
     uint64_t cert_base;            // global index of certificate 0 (z stream nonce)
     const uint32_t* keys_raw;      // [K][8] raw key words (as hashed)
     const uint32_t* key_info;      // [K]
-    const uint32_t* key_tab;       // [K][comb_words(key_window)]
-    const uint32_t* btab;          // [comb_words(16)] basepoint comb
+    const uint32_t* key_tab;       // [K][key_stride]: T+ (comb_words(key_window)), then T- when key_negtab
+    const uint32_t* btab;          // [B_TABLES][comb_words(B_WINDOW)] basepoint comb T+, then T- (B_NEGTAB)
+    uint64_t key_stride;           // u32 words per key-cache slot
+    uint32_t key_negtab;           // every key table is followed by its negated copy
     uint32_t zseed[8];
     uint32_t* flags;               // [n] NW_F_* bits
     uint32_t* slow_count;          // [1]
@@ -112,8 +114,10 @@ hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, c
 hipError_t launch_group_scatter(uint32_t n, uint32_t nkeys, const uint32_t* signer, const uint32_t* counts,
                                 uint32_t* cursor, uint32_t* perm, hipStream_t st);
 hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hipStream_t st);
+// Tables for nk keys at tab + j * stride (u32 words); negtab: each followed by its negated copy
+// (stride >= 2 comb_words(window)).
 hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
-                           uint32_t* tab, int window, hipStream_t st);
+                           uint32_t* tab, size_t stride, bool negtab, int window, hipStream_t st);
 hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* off, const uint64_t* len,
                               uint8_t* out, hipStream_t st);
 hipError_t launch_sign(uint32_t n, int msg_words, const uint32_t* seeds, const uint32_t* msgs,

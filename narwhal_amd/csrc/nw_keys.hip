@@ -22,7 +22,8 @@ __global__ void __launch_bounds__(64) k_key_prep(uint32_t nk, const uint32_t* ke
 static constexpr int COMB_CH = 8;
 
 template <int W>
-__global__ void __launch_bounds__(256) k_comb_build(uint32_t nk, const uint32_t* bases, uint32_t* tab) {
+__global__ void __launch_bounds__(256) k_comb_build(uint32_t nk, const uint32_t* bases, uint32_t* tab,
+                                                    size_t stride) {
     const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nch = (comb_ent(W) + COMB_CH - 1) / COMB_CH;
     const uint64_t per_key = (uint64_t)comb_pos(W) * nch;
@@ -30,7 +31,28 @@ __global__ void __launch_bounds__(256) k_comb_build(uint32_t nk, const uint32_t*
     const uint32_t j = (uint32_t)(gid / per_key);
     const uint64_t rem = gid % per_key;
     comb_chunk_build<W, COMB_CH>(bases + (size_t)j * comb_pos(W) * 40, (uint32_t)(rem / nch), (uint32_t)(rem % nch),
-                                 tab + (size_t)j * comb_words(W));
+                                 tab + (size_t)j * stride);
+}
+
+// The negated copy T- of each key's table, written right after it (tab + j * stride + comb_words(W)):
+// entry e of T- is -T[e] = ((y-x)/2, (y+x)/2, -d x y), d x y carried to tight limbs.  k_verify then
+// takes a signed digit's entry from T+ or T- by address, with no negation in the addition.
+template <int W>
+__global__ void __launch_bounds__(256) k_comb_negate(uint32_t nk, uint32_t* tab, size_t stride) {
+    const uint64_t gid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t per_key = (uint64_t)comb_pos(W) * comb_ent(W);
+    if (gid >= (uint64_t)nk * per_key) return;
+    const uint32_t* src = tab + (size_t)(gid / per_key) * stride + (size_t)(gid % per_key) * PRECOMP_WORDS;
+    const ge_precomp q = ge_precomp_from_words(src);
+    ge_precomp r;
+    r.ypx = q.ymx;
+    r.ymx = q.ypx;
+    r.xy2d = fe_carry(fe_neg(q.xy2d));
+    uint32_t w[PRECOMP_WORDS];
+    precomp_to_words(r, w);
+    uint4* dst = reinterpret_cast<uint4*>(const_cast<uint32_t*>(src) + comb_words(W));
+#pragma unroll
+    for (int k = 0; k < PRECOMP_WORDS / 4; ++k) dst[k] = make_uint4(w[4 * k], w[4 * k + 1], w[4 * k + 2], w[4 * k + 3]);
 }
 
 // ------------------------------------------------------------------------------------ signing
@@ -53,26 +75,31 @@ __global__ void __launch_bounds__(256) k_sign(uint32_t n, const uint32_t* seeds,
 
 template <int W>
 static hipError_t launch_key_prep_w(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
-                                    uint32_t* tab, hipStream_t st) {
+                                    uint32_t* tab, size_t stride, bool negtab, hipStream_t st) {
     hipLaunchKernelGGL(k_key_prep<W>, dim3(blocks_for(nk, 64)), dim3(64), 0, st, nk, keys_raw, key_info, bases);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t total = (uint64_t)nk * comb_pos(W) * ((comb_ent(W) + COMB_CH - 1) / COMB_CH);
-    hipLaunchKernelGGL(k_comb_build<W>, dim3(blocks_for(total, 256)), dim3(256), 0, st, nk, bases, tab);
+    hipLaunchKernelGGL(k_comb_build<W>, dim3(blocks_for(total, 256)), dim3(256), 0, st, nk, bases, tab, stride);
+    e = hipGetLastError();
+    if (e != hipSuccess || !negtab) return e;
+    const uint64_t ents = (uint64_t)nk * comb_pos(W) * comb_ent(W);
+    hipLaunchKernelGGL(k_comb_negate<W>, dim3(blocks_for(ents, 256)), dim3(256), 0, st, nk, tab, stride);
     return hipGetLastError();
 }
 
 hipError_t launch_key_prep(uint32_t nk, const uint32_t* keys_raw, uint32_t* key_info, uint32_t* bases,
-                           uint32_t* tab, int window, hipStream_t st) {
+                           uint32_t* tab, size_t stride, bool negtab, int window, hipStream_t st) {
     if (nk == 0) return hipSuccess;
-    if (window == B_WINDOW) return launch_key_prep_w<B_WINDOW>(nk, keys_raw, key_info, bases, tab, st);
+    if (window < 8 || window > B_WINDOW || stride < comb_words(window) * (negtab ? 2 : 1)) return hipErrorInvalidValue;
+    if (window == B_WINDOW) return launch_key_prep_w<B_WINDOW>(nk, keys_raw, key_info, bases, tab, stride, negtab, st);
     switch (window) {
-        case 8: return launch_key_prep_w<8>(nk, keys_raw, key_info, bases, tab, st);
-        case 9: return launch_key_prep_w<9>(nk, keys_raw, key_info, bases, tab, st);
-        case 12: return launch_key_prep_w<12>(nk, keys_raw, key_info, bases, tab, st);
-        case 13: return launch_key_prep_w<13>(nk, keys_raw, key_info, bases, tab, st);
-        case 16: return launch_key_prep_w<16>(nk, keys_raw, key_info, bases, tab, st);
-        case 20: return launch_key_prep_w<20>(nk, keys_raw, key_info, bases, tab, st);
+        case 8: return launch_key_prep_w<8>(nk, keys_raw, key_info, bases, tab, stride, negtab, st);
+        case 9: return launch_key_prep_w<9>(nk, keys_raw, key_info, bases, tab, stride, negtab, st);
+        case 12: return launch_key_prep_w<12>(nk, keys_raw, key_info, bases, tab, stride, negtab, st);
+        case 13: return launch_key_prep_w<13>(nk, keys_raw, key_info, bases, tab, stride, negtab, st);
+        case 16: return launch_key_prep_w<16>(nk, keys_raw, key_info, bases, tab, stride, negtab, st);
+        case 20: return launch_key_prep_w<20>(nk, keys_raw, key_info, bases, tab, stride, negtab, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -48,6 +48,13 @@ NW_HD constexpr size_t comb_words(int w) { return (size_t)comb_pos(w) * comb_ent
 #define NW_BW 24
 #endif
 static constexpr int B_WINDOW = NW_BW;
+// The basepoint table carries its negated copy (k_verify's basepoint pass picks entries by address,
+// no negation) while both fit comfortably: 2 x 11.8 GB at W24; at W26 (42.9 GB) the copy is left out.
+#ifndef NW_BASE_NEGTAB
+#define NW_BASE_NEGTAB (NW_BW <= 24)
+#endif
+static constexpr bool B_NEGTAB = NW_BASE_NEGTAB;
+static constexpr int B_TABLES = B_NEGTAB ? 2 : 1;
 
 NW_HD ge_p3 ge_identity() {
     ge_p3 r;
@@ -177,6 +184,32 @@ NW_HD madd_mid ge_madd_s1_sgn(const ge_p3& p, const ge_precomp& q, uint32_t m) {
 template <bool FUSED = false>
 NW_HD ge_p3 ge_madd_sgn(const ge_p3& p, const ge_precomp& q, uint32_t m) {
     return ge_madd_s2<FUSED>(ge_madd_s1_sgn<FUSED>(p, q, m));
+}
+
+// The chain's last addition: X, Y, Z only (T = e h is not needed by k_verify's checks; the rare
+// lane that parks P for the exact path rescales instead, p3_from_xyz).  Saves one of the 162 FMs.
+template <bool FUSED>
+NW_HD ge_p3 ge_madd_s2_xyz(const madd_mid& m) {
+    ge_p3 r;
+    if constexpr (FUSED) {
+        fe_mul3(r.X, m.e, m.f, r.Y, m.g, m.h, r.Z, m.g, m.f);
+    } else {
+        r.X = fe_mul(m.e, m.f);
+        r.Y = fe_mul(m.g, m.h);
+        r.Z = fe_mul(m.g, m.f);
+    }
+    r.T = fe_zero();   // not computed
+    return r;
+}
+
+// (X : Y : Z) -> extended (X Z : Y Z : Z^2 : X Y), the same point with T = X Y / Z.
+NW_HD ge_p3 p3_from_xyz(const ge_p3& p) {
+    ge_p3 r;
+    r.X = fe_mul(p.X, p.Z);
+    r.Y = fe_mul(p.Y, p.Z);
+    r.Z = fe_sq(p.Z);
+    r.T = fe_mul(p.X, p.Y);
+    return r;
 }
 
 // Extended point of a halved affine Niels entry, with no field multiplication beyond T:

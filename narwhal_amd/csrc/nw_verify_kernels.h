@@ -42,9 +42,12 @@ __device__ __forceinline__ bool lane_inputs(const VerifyParams& a, uint32_t i, u
 // A signature whose y does not match R's (so D_i = R_i - P_i != O: it will take the exact batch
 // path) parks its P_i for k_slow_prep, which would otherwise recompute h_i and both combs.  Rare:
 // honest batches never take the branch.
+// HAS_T false: P carries X, Y, Z only (k_verify's last addition skips T): parked rescaled.
+template <bool HAS_T = true>
 __device__ __forceinline__ uint32_t park_mismatch(const VerifyParams& a, uint32_t i, const ge_p3& P, uint32_t pf) {
     if (a.batch_mode && a.pslow && !(pf & PF_YMATCH) && (pf & (NW_F_S_OK | NW_F_A_OK)) == (NW_F_S_OK | NW_F_A_OK)) {
-        store_p3(a.pslow + (size_t)i * 40, P);
+        if constexpr (HAS_T) store_p3(a.pslow + (size_t)i * 40, P);
+        else store_p3(a.pslow + (size_t)i * 40, p3_from_xyz(P));
         pf |= NW_F_P_SAVED;
     }
     return pf;
@@ -62,7 +65,9 @@ __device__ __forceinline__ uint32_t park_mismatch(const VerifyParams& a, uint32_
 #ifndef NW_VERIFY_WAVES
 #define NW_VERIFY_WAVES 3
 #endif
-template <int MSGMODE, int WA>
+// NT: the key tables carry their negated copies (VerifyParams::key_negtab); the basepoint's does when
+// B_NEGTAB.
+template <int MSGMODE, int WA, bool NT>
 __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_verify(VerifyParams a) {
     const uint32_t gid = a.g0 + blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= a.g0 + a.gn) return;
@@ -99,13 +104,13 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
         for (int p = 0; p < NA; ++p) digs[(NB + p) * 256 + threadIdx.x] = next_digit<WA>(h, carry);
     }
     ge_p3 P;
-    comb_pass_dig<B_WINDOW, true, MSGMODE == 0 && NW_MADD_FUSED>(P, digs + threadIdx.x, 256, a.btab, false);
-    comb_pass_dig<WA, false, MSGMODE == 0 && NW_MADD_FUSED>(P, digs + NB * 256 + threadIdx.x, 256,
-                                                           a.key_tab + (size_t)slot * comb_words(WA), true);
+    comb_pass_dig<B_WINDOW, true, MSGMODE == 0 && NW_MADD_FUSED, B_NEGTAB>(P, digs + threadIdx.x, 256, a.btab, false);
+    comb_pass_dig<WA, false, MSGMODE == 0 && NW_MADD_FUSED, NT, true>(P, digs + NB * 256 + threadIdx.x, 256,
+                                                               a.key_tab + (size_t)slot * a.key_stride, true);
 #else
     // fused-carry products only in the 3-waves-per-SIMD kernel (MSGMODE 0); see ge_madd_s1
     const ge_p3 P = compute_P<WA, B_WINDOW, MSGMODE == 0 && NW_MADD_FUSED>(S, h, sok, a.btab,
-                                                                           a.key_tab + (size_t)slot * comb_words(WA));
+                                                                           a.key_tab + (size_t)slot * a.key_stride);
 #endif
     // X, Z and the partial flags (y match, R sign, R small) in processing order, struct-of-arrays
     // (column gid): coalesced for k_finish, which completes the flags and writes flags[i].  R, i
@@ -115,7 +120,7 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     asm volatile("" ::: "memory");
     const uint32_t i2 = a.perm ? a.perm[gid] : gid;
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i2 * 16);
-    store_prec_soa(a.pbuf, a.n, gid, P, park_mismatch(a, i2, P, verify_pflags(P, R, frow[gid])));
+    store_prec_soa(a.pbuf, a.n, gid, P, park_mismatch<!NW_DIG_LDS>(a, i2, P, verify_pflags(P, R, frow[gid])));
 }
 
 // Latency-mode kernel for small launches (nw_verify_split.h, compiled in nw_kvs.hip).
@@ -184,7 +189,7 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
         } else {   // y matched but x's sign did not (R = -P): recompute P
             uint32_t R2[8], S[8], h[8], slot, kinfo, c2;
             lane_inputs<MSGMODE>(a, i, R2, S, slot, kinfo, c2, h);
-            P = compute_P<WA>(S, h, true, a.btab, a.key_tab + (size_t)slot * comb_words(WA));
+            P = compute_P<WA>(S, h, true, a.btab, a.key_tab + (size_t)slot * a.key_stride);
         }
 #ifdef NW_SLOW_TIMING
         const uint64_t tm2 = __builtin_amdgcn_s_memtime();
@@ -234,10 +239,12 @@ hipError_t launch_vs_wa(const VerifyParams& p, int msgmode, bool slow, uint32_t 
     if (!slow && p.gn <= VERIFY_SPLIT_MAX_SIGS) return launch_split_wa<WA>(p, msgmode, st);
     if (msgmode == 0) {
         if (slow) hipLaunchKernelGGL((k_slow_prep<0, WA>), g, b, 0, st, p);
-        else hipLaunchKernelGGL((k_verify<0, WA>), g, b, 0, st, p);
+        else if (p.key_negtab) hipLaunchKernelGGL((k_verify<0, WA, true>), g, b, 0, st, p);
+        else hipLaunchKernelGGL((k_verify<0, WA, false>), g, b, 0, st, p);
     } else {
         if (slow) hipLaunchKernelGGL((k_slow_prep<1, WA>), g, b, 0, st, p);
-        else hipLaunchKernelGGL((k_verify<1, WA>), g, b, 0, st, p);
+        else if (p.key_negtab) hipLaunchKernelGGL((k_verify<1, WA, true>), g, b, 0, st, p);
+        else hipLaunchKernelGGL((k_verify<1, WA, false>), g, b, 0, st, p);
     }
     return hipGetLastError();
 }

@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
     const int p0 = (int)j * K;
     for (int q = 0; q < p0 && q < PB; ++q) shift_window<WB>(sp);
     for (int q = PB; q < p0; ++q) shift_window<WA>(hp);
-    const uint32_t* atab = a.key_tab + (size_t)slot * comb_words(WA);
+    const uint32_t* atab = a.key_tab + (size_t)slot * a.key_stride;
     // all K digits first (cheap shifts), so each table entry's 128-B gather can be issued one
     // position ahead, under the previous mixed addition (the entries are cold in L2: a lone
     // signature's chain would otherwise wait a full memory round trip per position)

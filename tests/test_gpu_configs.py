@@ -57,6 +57,7 @@ class TestC2W20:
     def test_c2_committee_mode_is_w20(self, c2):
         eng, com, slots, cs = c2
         assert eng.key_window() == 20 and eng.committee_size() == 100
+        assert eng.key_negtab()   # 2 x 1.25 x 100 W20 tables fit the budget: the negated copies
         assert cs.nsigs == 1000042
 
     def test_c2_w20_all_valid(self, c2):

@@ -1,0 +1,79 @@
+"""Key tables with and without their negated copies (nw_key_negtab): k_verify<MSGMODE, WA, NT>
+reads a signed digit's entry from T+ or T- by address when the copies exist, and negates T+ entries
+in the addition when they do not (NWCRYPTO_KEY_NEGTAB=0, or a cache too large for twice the
+tables).  Both kernels, in both message modes, must give the oracle's verdicts bit for bit.
+
+40,200 signatures per call: above VERIFY_SPLIT_MAX_SIGS (16,384), so the throughput kernel runs,
+not the latency split kernel.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import nw_ref
+
+pytestmark = pytest.mark.gpu
+
+ZSEED = bytes(range(32))
+THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+VALIDATORS, NCERTS, VOTES = 200, 600, 67
+
+
+@pytest.fixture(scope="module")
+def workload_200():
+    from narwhal_amd import _lib, workload
+    eng = _lib.Engine(device=0)
+    com = workload.make_committee(VALIDATORS, eng)
+    cs = workload.make_certificates(com, NCERTS, VOTES, eng)
+    eng.close()
+    rng = np.random.default_rng(11)
+    sigs = cs.sigs.copy()
+    bad = rng.choice(cs.nsigs, 120, replace=False)
+    for j, b in enumerate(bad):
+        if j % 3 == 0:
+            sigs[b, 40] ^= 1          # S changed: the equation fails
+        elif j % 3 == 1:
+            sigs[b, 3] ^= 0x10        # R changed
+        else:
+            sigs[b, 63] |= 0xE0       # S not canonical
+    return com, cs, sigs, bad
+
+
+def _run(negtab, window, com, cs, sigs, monkeypatch):
+    from narwhal_amd import _lib
+    monkeypatch.setenv("NWCRYPTO_KEY_NEGTAB", "1" if negtab else "0")
+    eng = _lib.Engine(device=0, key_window=window)
+    try:
+        slots = np.asarray(eng.committee_load_np(com.pks, com.stake), np.uint32)
+        assert eng.key_negtab() == negtab and eng.key_window() == window
+        cert = eng.verify_certs_np(cs.cert_first, cs.cert_n, sigs, slots[cs.signer], cs.msgs, ZSEED, 0)
+        # MSGMODE 1 (per-signature messages): each vote's message is its certificate digest
+        per_sig = np.repeat(cs.msgs, cs.cert_n, axis=0)
+        bat = eng.verify_batches_np(cs.cert_first, cs.cert_n, per_sig, slots[cs.signer], sigs, ZSEED, 0)
+    finally:
+        eng.close()
+    return cert, bat
+
+
+@pytest.mark.parametrize("window", [12, 16])
+def test_negtab_and_plain_tables_match_oracle(workload_200, window, monkeypatch):
+    com, cs, sigs, bad = workload_200
+    (ok1, sig1, st1), (bok1, bsig1) = _run(True, window, com, cs, sigs, monkeypatch)
+    (ok0, sig0, st0), (bok0, bsig0) = _run(False, window, com, cs, sigs, monkeypatch)
+    exp_sig = np.ones(cs.nsigs, bool)
+    exp_sig[bad] = False
+    exp_cert = np.ones(cs.ncerts, bool)
+    exp_cert[sorted(set((bad // VOTES).tolist()))] = False
+    for sig_ok in (sig1, sig0, bsig1, bsig0):
+        assert (sig_ok.astype(bool) == exp_sig).all()
+    for cert_ok in (ok1, ok0, bok1, bok0):
+        assert (cert_ok.astype(bool) == exp_cert).all()
+    assert (st1 == st0).all()
+    # the batch equation itself against the oracle, same coefficients
+    import copy
+    cs2 = copy.copy(cs)
+    cs2.sigs = sigs
+    sel = list(range(0, cs.ncerts, 7)) + sorted(set((bad // VOTES).tolist()))
+    want = nw_ref.verify_certs(cs2, com, sel, ZSEED, THREADS)
+    assert [bool(ok1[c]) for c in sel] == want
