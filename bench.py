@@ -60,9 +60,10 @@ def kverify_fm_per_sig(key_window, base_window=B_WINDOW):
     addition per comb digit position of s (basepoint comb) and of h (key comb), no doublings,
     except the chain's first entry, which is converted to extended coordinates with ONE
     multiplication (T = X*Y) instead of being added to the identity (nw_core.h comb_pass_dig<...,
-    true, ...>).  C2 (W24 + W20): 7 x (11 + 13 - 1) + 1 = 162.  The SHA-512 block, mod-l reduction
-    and digit recoding are VALU work not counted here."""
-    return MADD_FM * (comb_pos(base_window) + comb_pos(key_window) - 1) + 1
+    true, ...>), and the chain's last addition, which skips T = e*h (6 FM, comb_pass_dig<..., LAST>).
+    C2 (W24 + W20): 7 x (11 + 13 - 1) + 1 - 1 = 161.  The SHA-512 block, mod-l reduction and digit
+    recoding are VALU work not counted here."""
+    return MADD_FM * (comb_pos(base_window) + comb_pos(key_window) - 1) + 1 - 1
 
 
 def valu_peak_mad_per_s():
@@ -87,16 +88,17 @@ def traffic_per_launch():
 
 def clock_frac_profile():
     """k_verify's fraction of the MAD peak per shader cycle (both kernels timed in cycles by PMC
-    GRBM_GUI_ACTIVE: a gpu_pmc.sh pass + tools/clock_frac.py -> profiles/r04/clock_frac_r04h.json)."""
-    path = os.path.join(ROOT, "profiles", "r04", "clock_frac_r04h.json")
+    GRBM_GUI_ACTIVE: gpu_pmc.sh passes -> profiles/r05/clock_frac_r05.json; the MAD peak per cycle from
+    tools/valu_peak under the same counter, profiles/r04/clock_frac_r04h.json)."""
+    path = os.path.join(ROOT, "profiles", "r05", "clock_frac_r05.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
     return {"frac_per_cycle": d["frac_per_cycle"], "peak_mad_per_cycle": d["peak_mad_per_cycle"],
             "kverify_alg_mad_per_cycle": d["kverify_alg_mad_per_cycle"],
-            "source": "profiles/r04/clock_frac_r04h.json (PMC GRBM_GUI_ACTIVE on tools/valu_peak and on k_verify "
-                      "at C2, same 162-FM work model)"}
+            "source": "profiles/r05/clock_frac_r05.json (PMC GRBM_GUI_ACTIVE on k_verify at C2, same 161-FM work "
+                      "model; peak per cycle: tools/valu_peak, profiles/r04/clock_frac_r04h.json)"}
 
 
 def host_cores():
@@ -266,10 +268,10 @@ def host_fed(eng, cs, slots, zseed, chunks=16, threads=8, reps=5, stream_passes=
 
     value: STREAMING, the calls of ``stream_passes`` passes submitted back to back on the same threads
     (a node's Core keeps submitting as batches arrive; no barrier between passes).  passes: the same
-    calls with a barrier after every pass (ms_reps), on reused and on freshly allocated buffers.  About
-    one pass in three to five takes 5-13 ms longer: every calling thread blocks inside hipMemcpyAsync
-    (pinned source) while the GPU idles (HIP API trace, profiles/r05/host_fed_r05.txt); an SDMA-side
-    stall of the runtime (gone with HSA_ENABLE_SDMA=0, whose blit-kernel copies halve the throughput)."""
+    calls with a barrier after every pass (ms_reps), on reused and on freshly allocated buffers.  Copy
+    stalls (every calling thread inside hipMemcpyAsync for 5-13 ms while the GPU idles: HIP API trace,
+    profiles/r05/host_fed_r05.txt) concentrate in the first streaming round after start-up, so one
+    untimed streaming round runs first."""
     from concurrent.futures import ThreadPoolExecutor
     import numpy as np
     bounds = np.linspace(0, cs.ncerts, chunks + 1).astype(int)
@@ -289,7 +291,13 @@ def host_fed(eng, cs, slots, zseed, chunks=16, threads=8, reps=5, stream_passes=
     fresh_sets = [fresh(parts) for _ in range(reps)]
     stream_sets = [fresh(parts) for _ in range(4)]
     with ThreadPoolExecutor(threads) as ex:
-        assert all(ex.map(run, parts))   # warm every workspace
+        # warm-up, untimed: one streaming round over every set.  The first streaming round after
+        # start-up stalls (16-48 of its 320 calls take 5-11 ms, every thread inside hipMemcpyAsync
+        # with the GPU idle: 212-304 M sigs/s); every later round runs clean at 434-500 M with no call
+        # over 5 ms (tools/host_fed_stream_probe.py, profiles/r05/host_fed_r05.txt).  The workspace
+        # pool is already full-sized after the single-pass warm-up, so the stall is start-up state
+        # of the runtime's copy path; a running node is past it.
+        assert all(ex.map(run, [p for k in range(stream_passes) for p in stream_sets[k % len(stream_sets)]]))
         t0 = time.perf_counter()
         ok = all(ex.map(run, [p for k in range(stream_passes) for p in stream_sets[k % len(stream_sets)]]))
         t_stream = time.perf_counter() - t0
@@ -314,7 +322,7 @@ def host_fed(eng, cs, slots, zseed, chunks=16, threads=8, reps=5, stream_passes=
                                          "ms_reps": [t * 1e3 for t in tf]}},
             "note": "nw_verify_certs on pageable host buffers (every input staged through the call's pinned buffer), "
                     "%d calls of ~%d signatures on %d threads; value: %d passes' calls streamed back to back on "
-                    "fresh host arrays (4 rotating sets); passes: a barrier after every pass, median of %d (reused "
+                    "fresh host arrays (4 rotating sets) after one untimed streaming round; passes: a barrier after every pass, median of %d (reused "
                     "arrays; fresh_buffers: newly allocated ones); PCIe and host packing included"
                     % (chunks, cs.nsigs // chunks, threads, stream_passes, reps)}
 
@@ -1058,7 +1066,8 @@ def main(argv=None):
                         "above: the timed launches, back to back%s)" % (
                             ", overlapping the other batch's kernels" if nst > 1 else "")},
             "work_model": "%.0f sigs/launch (%d launches per step) x %d FM/sig (7 FM per mixed addition x (%d basepoint "
-                          "+ %d key - 1) comb positions + 1 FM for the chain's first entry, key window %d) x 100 u32 "
+                          "+ %d key - 1) comb positions + 1 FM for the chain's first entry - 1 FM (no T in the last addition), key "
+                          "window %d) x 100 u32 "
                           "MADs; SHA-512/mod-l/recoding VALU work not counted; peak = measured v_mad_u64_u32 rate"
                           % (sigs_per_launch, kn // args.steps, fm, comb_pos(bw), comb_pos(kw), kw),
             "dalek_equiv": {"fm_per_sig": v1, "TMADps": (sigs_per_launch * v1 * MADS_PER_FM / avg_launch_s / 1e12)

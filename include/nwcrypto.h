@@ -86,8 +86,10 @@ typedef struct nw_opts {
                           10,000-validator committee; W9 up to ~216,000: the worker's 100,000 keys,
                           or its 200,000 declared through max_keys).  Table bytes per key: w8 0.53 MB,
                           w9 0.95 MB, w12 5.77 MB, w13 10.5 MB, w16 67.1 MB, w20 872 MB; additions per
-                          signature 32 / 29 / 22 / 20 / 16 / 13.  (The basepoint comb is fixed at w24:
-                          11 additions, 11.8 GB per context.) */
+                          signature 32 / 29 / 22 / 20 / 16 / 13; twice the bytes when the tables
+                          carry their negated copies (nw_key_negtab).  (The basepoint comb is fixed
+                          at w24: 11 additions; it and its negated copy, 23.6 GB, are shared by every
+                          context of the process on the same device.) */
 } nw_opts;
 
 /* One certificate: its votes are sig[first_vote .. first_vote + n_votes). */

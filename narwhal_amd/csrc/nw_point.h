@@ -25,13 +25,26 @@ struct ge_cached {
 };
 
 // Table entry layout in HBM: 32 u32 words = 128 B (one cache line):
-//   [0..9] (y+x)/2, [10..11] zero, [12..21] (y-x)/2, [22..31] d x y.
+//   [0..9] (y+x)/2, [10..11] zero, [12..21] (y-x)/2, [22..31] d x y, radix-2^25.5 limbs as words.
 // (y+x)/2 and (y-x)/2 both start 16-byte aligned, so a comb step loads them in either order by
 // address: the conditional negation of a signed digit (-q swaps the two and negates d x y) costs no
 // select between the gather and the first products (comb_pass_dig; the sign of d x y is applied
-// to the product T d x y instead, ge_madd_sgn).  Round 4's layout ([0..9] [10..19] [20..29], pad)
-// needed the entry whole before 30 selects: k_verify 1.12 ms at C2 against 0.95 without them.
+// to the product T d x y instead, ge_madd_sgn, or taken from the negated copy of the table,
+// k_comb_negate).  Round 4's layout ([0..9] [10..19] [20..29], pad) needed the entry whole before
+// 30 selects.
+// NW_PACKED_ENT=1 (variant builds): [0..7] (y+x)/2, [8..15] (y-x)/2, [16..23] d x y as canonical
+// 255-bit words, [24..31] unused: a gather touches 96 of the 128 bytes and unpacks the limbs after
+// the load (fe_frombytes_w, ~46 VALU per comb step).  Measured at C2 (profiles/r05/kverify_ab_r05.txt):
+// k_verify 1.092-1.113 ms packed vs 1.093-1.119 ms unpacked, i.e. no gain for 4% more VALU per
+// wave, so the unpacked layout stays the default.
+#ifndef NW_PACKED_ENT
+#define NW_PACKED_ENT 0
+#endif
+#if NW_PACKED_ENT
+static constexpr int ENT_YPX = 0, ENT_YMX = 8, ENT_XY2D = 16;
+#else
 static constexpr int ENT_YPX = 0, ENT_YMX = 12, ENT_XY2D = 22;
+#endif
 #ifndef NW_HALF_NIELS
 #define NW_HALF_NIELS 1
 #endif
@@ -412,17 +425,30 @@ NW_HD ge_precomp ge_precomp_cneg(const ge_precomp& q, bool neg) {
 
 NW_HD ge_precomp ge_precomp_from_words(const uint32_t* w) {
     ge_precomp q;
+#if NW_PACKED_ENT
+    q.ypx = fe_frombytes_w(w + ENT_YPX);
+    q.ymx = fe_frombytes_w(w + ENT_YMX);
+    q.xy2d = fe_frombytes_w(w + ENT_XY2D);
+#else
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
         q.ypx.v[i] = w[ENT_YPX + i];
         q.ymx.v[i] = w[ENT_YMX + i];
         q.xy2d.v[i] = w[ENT_XY2D + i];
     }
+#endif
     return q;
 }
 
 // The 32 words of a table entry (the layout above).
 NW_HD void precomp_to_words(const ge_precomp& q, uint32_t* w) {
+#if NW_PACKED_ENT
+    fe_tobytes_w(w + ENT_YPX, q.ypx);
+    fe_tobytes_w(w + ENT_YMX, q.ymx);
+    fe_tobytes_w(w + ENT_XY2D, q.xy2d);
+#pragma unroll
+    for (int i = 24; i < 32; ++i) w[i] = 0;
+#else
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
         w[ENT_YPX + i] = q.ypx.v[i];
@@ -431,6 +457,7 @@ NW_HD void precomp_to_words(const ge_precomp& q, uint32_t* w) {
     }
     w[10] = 0;
     w[11] = 0;
+#endif
 }
 
 // Table-entry (halved affine Niels) form of p (one inversion); tight limbs.

@@ -83,8 +83,8 @@ def test_config_plan_single_rank():
 
 
 def test_fm_work_model_matches_kernel_chain():
-    """k_verify executes 7 FM per comb position except the chain's first entry (1 FM):
-    C2 (W24 basepoint, W20 keys) = 7 x (11 + 13 - 1) + 1 = 162."""
+    """k_verify executes 7 FM per comb position except the chain's first entry (1 FM) and its last
+    addition (6 FM, no T): C2 (W24 basepoint, W20 keys) = 7 x (11 + 13 - 1) + 1 - 1 = 161."""
     import bench
-    assert bench.kverify_fm_per_sig(20, 24) == 162
-    assert bench.kverify_fm_per_sig(16, 24) == 7 * (11 + 16 - 1) + 1
+    assert bench.kverify_fm_per_sig(20, 24) == 161
+    assert bench.kverify_fm_per_sig(16, 24) == 7 * (11 + 16 - 1)
