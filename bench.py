@@ -674,6 +674,7 @@ def parse_args(argv):
                          "bounds its latency but not the step")
     ap.add_argument("--timing-only", action="store_true", help=argparse.SUPPRESS)   # A/B of timing-only variants
     ap.add_argument("--hw-queues", type=int, default=0, help="set GPU_MAX_HW_QUEUES (<= 32) before HIP starts")
+    ap.add_argument("--engine-flags", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)   # nw_opts.flags (A/B)
     ap.add_argument("--key-window", type=int, default=-1,
                     help="key comb window; -1 = committee mode (library sizes it for the loaded committee)")
     ap.add_argument("--dry-run", action="store_true",
@@ -851,7 +852,7 @@ def main(argv=None):
 
     from narwhal_amd import _lib, workload
     plan = config_plan(args, world, rank)
-    eng = _lib.Engine(device=local, key_window=args.key_window)
+    eng = _lib.Engine(device=local, key_window=args.key_window, flags=args.engine_flags)
     com = workload.make_committee(plan["validators"], eng)
     slots = eng.committee_load_np(com.pks, com.stake)
     first_cert = plan["first_cert"]                     # each rank: its own shard of certificates

@@ -67,9 +67,15 @@ extern "C" {
 
 typedef struct nw_ctx nw_ctx;
 
+/* nw_opts.flags */
+#define NW_OPT_NO_KEY_NEGTAB 0x1u     /* never store the key tables' negated copies (half the HBM per key;
+                                         k_verify's key pass then negates entries in the addition) */
+#define NW_OPT_CONTIGUOUS_TABLES 0x2u /* allocate the comb tables as physically contiguous HBM
+                                         (hipDeviceMallocContiguous, plain allocation if that fails) */
+
 typedef struct nw_opts {
     int device;        /* HIP device ordinal (one process per GPU; -1 = current device) */
-    uint32_t flags;    /* reserved, 0 */
+    uint32_t flags;    /* NW_OPT_* bits below; other bits are reserved (NW_ERR_ARG) */
     size_t max_keys;   /* key-cache capacity in keys.  0 = as many as the key budget holds.  The key
                           budget is the HBM free on the device at the first nw_committee_load (after
                           this context's basepoint table and anything other contexts or processes
@@ -88,8 +94,8 @@ typedef struct nw_opts {
                           w9 0.95 MB, w12 5.77 MB, w13 10.5 MB, w16 67.1 MB, w20 872 MB; additions per
                           signature 32 / 29 / 22 / 20 / 16 / 13; twice the bytes when the tables
                           carry their negated copies (nw_key_negtab).  (The basepoint comb is fixed
-                          at w24: 11 additions; it and its negated copy, 23.6 GB, are shared by every
-                          context of the process on the same device.) */
+                          at w24: 11 additions, 11.8 GB, shared by every context of the process on
+                          the same device.) */
 } nw_opts;
 
 /* One certificate: its votes are sig[first_vote .. first_vote + n_votes). */

@@ -130,13 +130,17 @@ def _buf(b: bytes):
 POINT_BYTES = 160   # NW_POINT_BYTES
 
 
+NW_OPT_NO_KEY_NEGTAB = 0x1
+NW_OPT_CONTIGUOUS_TABLES = 0x2
+
+
 class Engine:
     """One nw_ctx (one GPU).  Thread-safe and reentrant: every call leases its own stream and
     scratch in the C layer, so calls from several threads run concurrently."""
 
-    def __init__(self, device: int = -1, max_keys: int = 0, key_window: int = 0):
+    def __init__(self, device: int = -1, max_keys: int = 0, key_window: int = 0, flags: int = 0):
         self._ctx = ctypes.c_void_p()
-        opts = NwOpts(device, 0, max_keys, key_window)
+        opts = NwOpts(device, flags, max_keys, key_window)
         rc = LIB.nw_ctx_create(ctypes.byref(self._ctx), ctypes.byref(opts))
         if rc != NW_OK:
             raise DeviceError("nw_ctx_create failed (rc=%d): no usable gfx950 GPU" % rc)

@@ -179,6 +179,7 @@ struct nw_ctx {
     bool budget_fixed = false;    // window, max_keys and reservation decided (first load with keys)
     size_t key_words = 0;         // u32 words per key-cache slot (T+, and T- when key_negtab)
     bool key_negtab = false;      // each key table followed by its negated copy (k_verify: no negation)
+    uint32_t opt_flags = 0;       // nw_opts.flags (NW_OPT_*)
     size_t nkeys = 0, key_cap = 0;
     uint32_t* d_keys_raw = nullptr;
     uint32_t* d_key_info = nullptr;
@@ -415,18 +416,27 @@ void fix_window(nw_ctx* ctx, size_t first_load) {
     // Negated copies (T-) of the key tables when twice the tables still fit the budget for the keys
     // this context is sized for: k_verify's key pass then needs no conditional negation (7% of its
     // time at C2).  A large worker cache keeps the wider window instead (2 fewer comb positions are
-    // worth more than the negation).  NWCRYPTO_KEY_NEGTAB=0 turns it off (A/B).
+    // worth more than the negation).  NW_OPT_NO_KEY_NEGTAB turns it off.
     // (sized for: the declared max_keys, else the first load with committee mode's 25% headroom; an
     // automatic window leaves room for 4x the first load)
     const double sized = ctx->max_keys_user ? (double)std::max(ctx->max_keys, first_load)
                                             : (double)first_load * (auto_window ? 4.0 : 1.25);
-    const char* env = getenv("NWCRYPTO_KEY_NEGTAB");
-    ctx->key_negtab = !(env && env[0] == '0') &&
+    ctx->key_negtab = !(ctx->opt_flags & NW_OPT_NO_KEY_NEGTAB) &&
                       2.0 * sized * (double)comb_words(ctx->key_window) * 4.0 <= (double)budget;
     ctx->key_words = comb_words(ctx->key_window) * (ctx->key_negtab ? 2 : 1);
     ctx->key_reserve = ctx->max_keys_user && ctx->committee_mode;
     ctx->budget_fixed = true;
     if (!ctx->max_keys_user) ctx->max_keys = budget / (ctx->key_words * 4);
+}
+
+// Comb-table allocation: physically contiguous HBM on request (NW_OPT_CONTIGUOUS_TABLES; larger
+// page fragments for the table gathers), else / on failure the plain allocation.
+hipError_t table_alloc(const nw_ctx* ctx, uint32_t** p, size_t bytes) {
+    if ((ctx->opt_flags & NW_OPT_CONTIGUOUS_TABLES) &&
+        hipExtMallocWithFlags(reinterpret_cast<void**>(p), bytes, hipDeviceMallocContiguous) == hipSuccess)
+        return hipSuccess;
+    (void)hipGetLastError();
+    return hipMalloc(p, bytes);
 }
 
 int grow_keys(nw_ctx* ctx, size_t need) {
@@ -449,7 +459,7 @@ int grow_keys(nw_ctx* ctx, size_t need) {
     hipError_t e = hipMalloc(&raw, cap * 32);
     if (e == hipSuccess) e = hipMalloc(&info, cap * 4);
     if (e == hipSuccess) e = hipMalloc(&stake, cap * 4);
-    if (e == hipSuccess) e = hipMalloc(&tab, cap * ctx->key_words * 4);
+    if (e == hipSuccess) e = table_alloc(ctx, &tab, cap * ctx->key_words * 4);
     if (e == hipSuccess && ctx->nkeys) {
         e = hipMemcpyAsync(raw, ctx->d_keys_raw, ctx->nkeys * 32, hipMemcpyDeviceToDevice, ctx->stream);
         if (e == hipSuccess)
@@ -1214,7 +1224,7 @@ int acquire_base(nw_ctx* ctx) {
         uint32_t* d_braw = nullptr;
         uint32_t* d_binfo = nullptr;
         int rc = NW_OK;
-        if (hipMalloc(&tab, B_TABLES * comb_words(B_WINDOW) * 4) != hipSuccess || hipMalloc(&d_braw, 32) != hipSuccess ||
+        if (table_alloc(ctx, &tab, B_TABLES * comb_words(B_WINDOW) * 4) != hipSuccess || hipMalloc(&d_braw, 32) != hipSuccess ||
             hipMalloc(&d_binfo, 16) != hipSuccess)
             rc = NW_ERR_NOMEM;
         if (rc == NW_OK && hipMemcpy(d_braw, kBaseEnc, 32, hipMemcpyHostToDevice) != hipSuccess) rc = NW_ERR_DEVICE;
@@ -1257,12 +1267,14 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     int dev = opts && opts->device >= 0 ? opts->device : -1;
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_DEVICE;
     if (dev >= ndev) return NW_ERR_ARG;
+    if (opts && (opts->flags & ~(NW_OPT_NO_KEY_NEGTAB | NW_OPT_CONTIGUOUS_TABLES))) return NW_ERR_ARG;
     if (opts && opts->key_window && opts->key_window != -1 && opts->key_window != 8 && opts->key_window != 9 &&
         opts->key_window != 12 && opts->key_window != 13 && opts->key_window != 16 && opts->key_window != 20)
         return NW_ERR_ARG;
     nw_ctx* ctx = new nw_ctx();
     ctx->device = dev;
     ctx->finish_k = NW_FK_FIXED;
+    if (opts) ctx->opt_flags = opts->flags;
     if (opts && opts->max_keys) {
         ctx->max_keys = opts->max_keys;
         ctx->max_keys_user = true;

@@ -289,18 +289,23 @@ __device__ __forceinline__ void comb_pass_dig(ge_p3& P, const int* dig, int stri
         else P = ent_sw_first(e0, neg0);
         pos = 1;
     }
+    auto add = [&](const ent_sw& e, bool n) {
+        if constexpr (NT) P = ge_madd<FUSED>(P, ent_sw_precomp(e));
+        else P = ge_madd_sgn<FUSED>(P, ent_sw_precomp(e), lane_mask(n));
+    };
+    auto sign = [&](int dd) { return neg_pos ? dd > 0 : dd < 0; };
+    constexpr int END = comb_pos(W) - (LAST ? 1 : 0);   // positions [pos, END) take a full addition
 #pragma nounroll
-    for (; pos < comb_pos(W) - (LAST ? 1 : 0); ++pos) {
+    for (; pos < END; ++pos) {
         int dn = 0;
         bool ngn = false;
         ent_sw nxt;
         if (pos + 1 < comb_pos(W)) {
             dn = dig[(pos + 1) * stride];
-            ngn = neg_pos ? dn > 0 : dn < 0;
+            ngn = sign(dn);
             nxt = gather(pos + 1, dn, ngn);
         }
-        if constexpr (NT) P = ge_madd<FUSED>(P, ent_sw_precomp(cur));
-        else P = ge_madd_sgn<FUSED>(P, ent_sw_precomp(cur), lane_mask(ng));
+        add(cur, ng);
         cur = nxt;
         d = dn;
         ng = ngn;

@@ -61,10 +61,12 @@ NW_HD constexpr size_t comb_words(int w) { return (size_t)comb_pos(w) * comb_ent
 #define NW_BW 24
 #endif
 static constexpr int B_WINDOW = NW_BW;
-// The basepoint table carries its negated copy (k_verify's basepoint pass picks entries by address,
-// no negation) while both fit comfortably: 2 x 11.8 GB at W24; at W26 (42.9 GB) the copy is left out.
+// NW_BASE_NEGTAB (variant builds): the basepoint table carries its negated copy too (+11.8 GB at W24),
+// so the basepoint pass also picks entries by address.  Measured in shader cycles per C2 k_verify launch
+// (PMC GRBM_GUI_ACTIVE, profiles/r05/pmc_ab_r05.txt): 2.00-2.14 M without the copy against 2.07-2.27 M
+// with it; the doubled table costs more than the 30 selects per basepoint step it saves.
 #ifndef NW_BASE_NEGTAB
-#define NW_BASE_NEGTAB (NW_BW <= 24)
+#define NW_BASE_NEGTAB 0
 #endif
 static constexpr bool B_NEGTAB = NW_BASE_NEGTAB;
 static constexpr int B_TABLES = B_NEGTAB ? 2 : 1;

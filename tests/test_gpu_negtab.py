@@ -1,7 +1,7 @@
 """Key tables with and without their negated copies (nw_key_negtab): k_verify<MSGMODE, WA, NT>
 reads a signed digit's entry from T+ or T- by address when the copies exist, and negates T+ entries
-in the addition when they do not (NWCRYPTO_KEY_NEGTAB=0, or a cache too large for twice the
-tables).  Both kernels, in both message modes, must give the oracle's verdicts bit for bit.
+in the addition when they do not (nw_opts.flags NW_OPT_NO_KEY_NEGTAB, or a cache too large for twice
+the tables).  Both kernels, in both message modes, must give the oracle's verdicts bit for bit.
 
 40,200 signatures per call: above VERIFY_SPLIT_MAX_SIGS (16,384), so the throughput kernel runs,
 not the latency split kernel.
@@ -40,10 +40,9 @@ def workload_200():
     return com, cs, sigs, bad
 
 
-def _run(negtab, window, com, cs, sigs, monkeypatch):
+def _run(negtab, window, com, cs, sigs):
     from narwhal_amd import _lib
-    monkeypatch.setenv("NWCRYPTO_KEY_NEGTAB", "1" if negtab else "0")
-    eng = _lib.Engine(device=0, key_window=window)
+    eng = _lib.Engine(device=0, key_window=window, flags=0 if negtab else _lib.NW_OPT_NO_KEY_NEGTAB)
     try:
         slots = np.asarray(eng.committee_load_np(com.pks, com.stake), np.uint32)
         assert eng.key_negtab() == negtab and eng.key_window() == window
@@ -57,10 +56,10 @@ def _run(negtab, window, com, cs, sigs, monkeypatch):
 
 
 @pytest.mark.parametrize("window", [12, 16])
-def test_negtab_and_plain_tables_match_oracle(workload_200, window, monkeypatch):
+def test_negtab_and_plain_tables_match_oracle(workload_200, window):
     com, cs, sigs, bad = workload_200
-    (ok1, sig1, st1), (bok1, bsig1) = _run(True, window, com, cs, sigs, monkeypatch)
-    (ok0, sig0, st0), (bok0, bsig0) = _run(False, window, com, cs, sigs, monkeypatch)
+    (ok1, sig1, st1), (bok1, bsig1) = _run(True, window, com, cs, sigs)
+    (ok0, sig0, st0), (bok0, bsig0) = _run(False, window, com, cs, sigs)
     exp_sig = np.ones(cs.nsigs, bool)
     exp_sig[bad] = False
     exp_cert = np.ones(cs.ncerts, bool)
