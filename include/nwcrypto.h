@@ -70,8 +70,6 @@ typedef struct nw_ctx nw_ctx;
 /* nw_opts.flags */
 #define NW_OPT_NO_KEY_NEGTAB 0x1u     /* never store the key tables' negated copies (half the HBM per key;
                                          k_verify's key pass then negates entries in the addition) */
-#define NW_OPT_CONTIGUOUS_TABLES 0x2u /* allocate the comb tables as physically contiguous HBM
-                                         (hipDeviceMallocContiguous, plain allocation if that fails) */
 
 typedef struct nw_opts {
     int device;        /* HIP device ordinal (one process per GPU; -1 = current device) */

@@ -130,8 +130,7 @@ def _buf(b: bytes):
 POINT_BYTES = 160   # NW_POINT_BYTES
 
 
-NW_OPT_NO_KEY_NEGTAB = 0x1
-NW_OPT_CONTIGUOUS_TABLES = 0x2
+NW_OPT_NO_KEY_NEGTAB = 0x1   # nw_opts.flags (include/nwcrypto.h)
 
 
 class Engine:

@@ -429,16 +429,6 @@ void fix_window(nw_ctx* ctx, size_t first_load) {
     if (!ctx->max_keys_user) ctx->max_keys = budget / (ctx->key_words * 4);
 }
 
-// Comb-table allocation: physically contiguous HBM on request (NW_OPT_CONTIGUOUS_TABLES; larger
-// page fragments for the table gathers), else / on failure the plain allocation.
-hipError_t table_alloc(const nw_ctx* ctx, uint32_t** p, size_t bytes) {
-    if ((ctx->opt_flags & NW_OPT_CONTIGUOUS_TABLES) &&
-        hipExtMallocWithFlags(reinterpret_cast<void**>(p), bytes, hipDeviceMallocContiguous) == hipSuccess)
-        return hipSuccess;
-    (void)hipGetLastError();
-    return hipMalloc(p, bytes);
-}
-
 int grow_keys(nw_ctx* ctx, size_t need) {
     if (need <= ctx->key_cap) return NW_OK;
     if (need > ctx->max_keys) {
@@ -459,7 +449,7 @@ int grow_keys(nw_ctx* ctx, size_t need) {
     hipError_t e = hipMalloc(&raw, cap * 32);
     if (e == hipSuccess) e = hipMalloc(&info, cap * 4);
     if (e == hipSuccess) e = hipMalloc(&stake, cap * 4);
-    if (e == hipSuccess) e = table_alloc(ctx, &tab, cap * ctx->key_words * 4);
+    if (e == hipSuccess) e = hipMalloc(&tab, cap * ctx->key_words * 4);
     if (e == hipSuccess && ctx->nkeys) {
         e = hipMemcpyAsync(raw, ctx->d_keys_raw, ctx->nkeys * 32, hipMemcpyDeviceToDevice, ctx->stream);
         if (e == hipSuccess)
@@ -1224,7 +1214,7 @@ int acquire_base(nw_ctx* ctx) {
         uint32_t* d_braw = nullptr;
         uint32_t* d_binfo = nullptr;
         int rc = NW_OK;
-        if (table_alloc(ctx, &tab, B_TABLES * comb_words(B_WINDOW) * 4) != hipSuccess || hipMalloc(&d_braw, 32) != hipSuccess ||
+        if (hipMalloc(&tab, B_TABLES * comb_words(B_WINDOW) * 4) != hipSuccess || hipMalloc(&d_braw, 32) != hipSuccess ||
             hipMalloc(&d_binfo, 16) != hipSuccess)
             rc = NW_ERR_NOMEM;
         if (rc == NW_OK && hipMemcpy(d_braw, kBaseEnc, 32, hipMemcpyHostToDevice) != hipSuccess) rc = NW_ERR_DEVICE;
@@ -1267,7 +1257,7 @@ int nw_ctx_create(nw_ctx** out, const nw_opts* opts) {
     int dev = opts && opts->device >= 0 ? opts->device : -1;
     if (dev < 0 && hipGetDevice(&dev) != hipSuccess) return NW_ERR_DEVICE;
     if (dev >= ndev) return NW_ERR_ARG;
-    if (opts && (opts->flags & ~(NW_OPT_NO_KEY_NEGTAB | NW_OPT_CONTIGUOUS_TABLES))) return NW_ERR_ARG;
+    if (opts && (opts->flags & ~NW_OPT_NO_KEY_NEGTAB)) return NW_ERR_ARG;
     if (opts && opts->key_window && opts->key_window != -1 && opts->key_window != 8 && opts->key_window != 9 &&
         opts->key_window != 12 && opts->key_window != 13 && opts->key_window != 16 && opts->key_window != 20)
         return NW_ERR_ARG;
