@@ -33,7 +33,7 @@ def main():
     durs = []
     with open(a.trace) as f:
         for row in csv.DictReader(f):
-            if re.match(r"void nw::k_verify<0, \d+>", row["Kernel_Name"]):
+            if re.match(r"void nw::k_verify<0, \d+(, (true|false))?>", row["Kernel_Name"]):
                 durs.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
     live = None
     kw, bw, sigs = a.key_window, a.base_window, a.sigs
