@@ -76,3 +76,35 @@ def test_negtab_and_plain_tables_match_oracle(workload_200, window):
     sel = list(range(0, cs.ncerts, 7)) + sorted(set((bad // VOTES).tolist()))
     want = nw_ref.verify_certs(cs2, com, sel, ZSEED, THREADS)
     assert [bool(ok1[c]) for c in sel] == want
+
+
+def test_shared_basepoint_table_outlives_the_first_context(workload_200):
+    """The basepoint comb is shared by the contexts of a process on a device (reference-counted):
+    a second engine verifies correctly while the first is alive and after the first is closed."""
+    from narwhal_amd import _lib
+    com, cs, sigs, bad = workload_200
+    sel = slice(0, 64)
+    first = np.asarray(cs.cert_first[sel], np.uint32)
+    n = np.asarray(cs.cert_n[sel], np.uint32)
+    nsig = int(first[-1] + n[-1])
+    e1 = _lib.Engine(device=0, key_window=12)
+    e2 = _lib.Engine(device=0, key_window=12)
+    try:
+        s1 = np.asarray(e1.committee_load_np(com.pks, com.stake), np.uint32)
+        s2 = np.asarray(e2.committee_load_np(com.pks, com.stake), np.uint32)
+        want = np.ones(len(n), bool)
+        want[sorted({int(b) // VOTES for b in bad if b < nsig})] = False
+        ok1, _, _ = e1.verify_certs_np(first, n, sigs[:nsig], s1[cs.signer[:nsig]], cs.msgs[sel], ZSEED, 0)
+        ok2, _, _ = e2.verify_certs_np(first, n, sigs[:nsig], s2[cs.signer[:nsig]], cs.msgs[sel], ZSEED, 0)
+        assert (ok1.astype(bool) == want).all() and (ok2.astype(bool) == want).all()
+        e1.close()
+        ok3, _, _ = e2.verify_certs_np(first, n, sigs[:nsig], s2[cs.signer[:nsig]], cs.msgs[sel], ZSEED, 0)
+        assert (ok3.astype(bool) == want).all()
+        e3 = _lib.Engine(device=0, key_window=12)   # re-acquires the live table
+        s3 = np.asarray(e3.committee_load_np(com.pks, com.stake), np.uint32)
+        ok4, _, _ = e3.verify_certs_np(first, n, sigs[:nsig], s3[cs.signer[:nsig]], cs.msgs[sel], ZSEED, 0)
+        assert (ok4.astype(bool) == want).all()
+        e3.close()
+    finally:
+        e2.close()
+        e1.close()
