@@ -731,7 +731,8 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     }
     NW_TRY(launch_verify(vp, msgmode, ctx->key_window, st), "k_verify");
     if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");   // brackets k_verify alone
-    NW_TRY(launch_finish(vp, st), "k_finish");
+    // small launches: k_verify_split has done k_finish's work itself (split_fuses_finish)
+    if (!split_fuses_finish(vp.gn, vp.fk)) NW_TRY(launch_finish(vp, st), "k_finish");
     if (!batch_mode) return NW_OK;   // strict verdicts only (bytes written by k_finish): no certificate pass
 
     NW_TRY(launch_slow(vp, msgmode, ctx->key_window, (uint32_t)nsigs, st), "k_slow_prep / k_slow_mul");

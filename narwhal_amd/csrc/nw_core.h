@@ -432,6 +432,27 @@ NW_HD uint32_t finish_x_flags(const fe& X, const fe& zi, uint32_t pf) {
     return finish_flags(pf, x_zero || ((xw[0] & 1u) == ((pf & PF_RSIGN) ? 1u : 0u)));
 }
 
+// A signature's final flags f (pf: its partial flags) stored, with the exact-path bookkeeping of a
+// batch call: a vote in no certificate's range gets no verdict; a parse / decode failure dooms its
+// certificate (dalek errors before the MSM); a mismatch joins the exact-path list.  k_finish, and
+// k_verify_split when it does k_finish's work itself (small launches).
+__device__ __forceinline__ void finish_emit(const VerifyParams& a, uint32_t i, uint32_t pf, uint32_t f) {
+    if (a.batch_mode) {
+        if (pf & PF_NOCERT) {
+            f = 0u;
+        } else if ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) {
+            atomicOr(&a.cert_state[a.sig_cert[i]], CS_DOOM);
+        } else if (!(f & NW_F_MATCH)) {
+            f |= NW_F_SLOW;
+            const uint32_t t = atomicAdd(a.slow_count, 1u);
+            a.slow_list[t] = i;
+            a.slow_slot[i] = t;
+        }
+    }
+    a.flags[i] = f;
+    if (a.ok_out) a.ok_out[i] = (f & NW_F_STRICT) ? 1 : 0;
+}
+
 // Flags from P (with zi = 1/Z_P) against the signature's R encoding (both halves).
 NW_HD uint32_t match_flags(const ge_p3& P, const fe& zi, const uint32_t R[8], bool sok, bool aok, bool asmall) {
     const uint32_t partial = (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | (asmall ? NW_F_A_SMALL : 0u);

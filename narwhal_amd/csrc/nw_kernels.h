@@ -39,6 +39,13 @@ static constexpr int PBUF_WORDS = 21;             // per-signature k_verify -> k
 #define NW_FINISH_K 16
 #endif
 static constexpr int FINISH_K = NW_FINISH_K;      // signatures per lane in the batch-inversion kernel
+#ifndef NW_INV_VAR
+#define NW_INV_VAR 1   // variable-time safegcd where the lanes' inversions are few (k_finish, fused split)
+#endif
+// Verify launches of at most this many signatures with one signature per k_finish lane (fk = 1) run
+// k_verify_split with k_finish's work fused in (nw_verify_split.h): no k_finish launch.
+static constexpr uint32_t SPLIT_FUSE_MAX_SIGS = 4096;
+inline bool split_fuses_finish(uint32_t gn, uint32_t fk) { return gn <= SPLIT_FUSE_MAX_SIGS && fk == 1; }
 
 static inline unsigned blocks_for(uint64_t n, unsigned t) { return (unsigned)((n + t - 1) / t); }
 

@@ -105,9 +105,6 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
 }
 
 // ------------------------------------------------------------------------------------ finish
-#ifndef NW_INV_VAR
-#define NW_INV_VAR 1
-#endif
 // Montgomery batch inversion of the Z of FINISH_K signatures per lane (one field inversion per
 // chunk), affine x, y, encoding match against R, strict verdict, and (batch mode) compaction of the
 // mismatching signatures into the exact-path list.  Lane L of NL owns the processing-order columns
@@ -128,25 +125,7 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
     const uint32_t cnt = (a.gn - L + NL - 1) / NL;   // columns g0 + L + k NL < g0 + gn  (cnt <= fk)
     const size_t n = a.n;
     const size_t gbase = (size_t)a.g0 + L;
-    // the verdict of column g (flags f): exact-path compaction (batch mode) and the stores
-    auto emit = [&](uint32_t i, uint32_t pf, uint32_t f) {
-        if (a.batch_mode) {
-            if (pf & PF_NOCERT) {
-                f = 0u;   // inside no certificate's range: no message, no verdict, no exact-path entry
-            } else if ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) {
-                // the certificate is rejected (dalek: parse / decode error before the MSM): no
-                // exact-path work for any of its votes
-                atomicOr(&a.cert_state[a.sig_cert[i]], CS_DOOM);
-            } else if (!(f & NW_F_MATCH)) {
-                f |= NW_F_SLOW;
-                const uint32_t t = atomicAdd(a.slow_count, 1u);
-                a.slow_list[t] = i;
-                a.slow_slot[i] = t;
-            }
-        }
-        a.flags[i] = f;
-        if (a.ok_out) a.ok_out[i] = (f & NW_F_STRICT) ? 1 : 0;
-    };
+    auto emit = [&](uint32_t i, uint32_t pf, uint32_t f) { finish_emit(a, i, pf, f); };
     if constexpr (ONE) {
         // one signature per lane: every load issued before the inversion, no prefix products
         const fe z = load_fe_soa(a.pbuf + 10 * n, n, gbase);

@@ -21,6 +21,7 @@ static constexpr int VERIFY_SPLIT = 8;
 // VERIFY_SPLIT_MAX_SIGS (nw_verify_kernels.h): the split grid is then <= two waves per SIMD
 // (1,024 SIMDs x 64 lanes x 2 / VERIFY_SPLIT)
 static_assert(VERIFY_SPLIT_MAX_SIGS * VERIFY_SPLIT <= 2 * 256 * 4 * 64, "split grid larger than two waves per SIMD");
+static_assert(SPLIT_FUSE_MAX_SIGS <= VERIFY_SPLIT_MAX_SIGS, "a fused launch must take the split kernel");
 
 // k + sum_{p < comb_pos(W)} 2^(W-1) 2^(W p) for k < 2^253 (< 2^(W comb_pos(W)) for every window).
 template <int W>
@@ -52,7 +53,11 @@ NW_HD int low_digit(const uint32_t kp[9]) {
     return (int)(kp[0] & ((1u << W) - 1u)) - (1 << (W - 1));
 }
 
-template <int MSGMODE, int WA>
+// FUSE (split_fuses_finish: launches of up to SPLIT_FUSE_MAX_SIGS signatures, one per k_finish lane):
+// after the butterfly every lane of a group holds P, so all 8 lanes run k_finish's work for their
+// signature (the inversion on a dense EXEC mask) and the group's first lane writes the verdict:
+// no k_finish launch and no P round trip through pbuf (a single header / vote check: ~5 us).
+template <int MSGMODE, int WA, bool FUSE>
 __global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
     constexpr int WB = B_WINDOW;
     constexpr int PB = comb_pos(WB), NPOS = PB + comb_pos(WA);
@@ -137,6 +142,13 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
         }
         P = ge_add(P, ge_to_cached(o));
     }
+    if constexpr (FUSE) {
+        const uint32_t pf = park_mismatch(a, i, P, verify_pflags(P, R, flags));
+        const fe zi = (NW_INV_VAR && a.gn <= 8) ? fe_invert_var(P.Z) : fe_invert_sg(P.Z);
+        const uint32_t f = finish_x_flags(P.X, zi, pf);
+        if (j == 0 && owner) finish_emit(a, i, pf, f);
+        return;
+    }
     if (j != 0 || !owner) return;
     store_prec_soa(a.pbuf, a.n, gid, P, park_mismatch(a, i, P, verify_pflags(P, R, flags)));
 }
@@ -144,8 +156,14 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
 template <int WA>
 hipError_t launch_split_wa(const VerifyParams& p, int msgmode, hipStream_t st) {
     const dim3 b(256), g(blocks_for((uint64_t)p.gn * VERIFY_SPLIT, 256));
-    if (msgmode == 0) hipLaunchKernelGGL((k_verify_split<0, WA>), g, b, 0, st, p);
-    else hipLaunchKernelGGL((k_verify_split<1, WA>), g, b, 0, st, p);
+    const bool fuse = split_fuses_finish(p.gn, p.fk);
+    if (msgmode == 0) {
+        if (fuse) hipLaunchKernelGGL((k_verify_split<0, WA, true>), g, b, 0, st, p);
+        else hipLaunchKernelGGL((k_verify_split<0, WA, false>), g, b, 0, st, p);
+    } else {
+        if (fuse) hipLaunchKernelGGL((k_verify_split<1, WA, true>), g, b, 0, st, p);
+        else hipLaunchKernelGGL((k_verify_split<1, WA, false>), g, b, 0, st, p);
+    }
     return hipGetLastError();
 }
 
