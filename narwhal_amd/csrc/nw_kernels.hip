@@ -186,15 +186,8 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
 // (parse / decode failure, all votes matching, one term with a prime-order component).  The rest
 // (two or more slow-path terms) is appended to the exact list for k_cert_exact, which has the
 // registers for the point sum: this kernel stays at a handful of VGPRs and never spills.
-__global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    if (a.sig_ok) {   // strict verdict bytes of every signature (the flags are final here)
-        const uint32_t nthr = gridDim.x * blockDim.x;
-        for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < a.nsigs; v += nthr)
-            a.sig_ok[v] = (a.flags[v] & NW_F_STRICT) ? 1 : 0;
-    }
-    if (c >= a.ncerts) return;   // whole wave exits together
+// Certificate c's finalize, by one wave (lane = 0..63).
+__device__ __forceinline__ void finalize_cert(const FinalizeParams& a, uint32_t c, uint32_t lane) {
     const uint32_t first = a.cert_first[c];
     // a vote range past the signature array (device inputs are not host-checked) rejects the
     // certificate; only the in-range votes are read
@@ -232,70 +225,105 @@ __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
     } else if ((a.cert_state[c] & CS_BIG_MASK) == 1u) {
         ok = false;   // one term with a prime-order component: the sum cannot be the identity (k_slow_prep)
     } else {
-        a.exact_list[atomicAdd(a.exact_count, 1u)] = c;   // k_cert_exact writes the verdict
+        a.exact_list[atomicAdd(a.exact_count, 1u)] = c;   // the exact sum writes the verdict
         return;
     }
     if (a.cert_ok) a.cert_ok[c] = ok ? 1 : 0;
 }
 
-// Exact sum of a listed certificate (one wave each, grid-stride over the list): every slow vote's
-// record holds its term z_i D_i (k_slow_mul for prime-order components, k_slow_prep's (z_i mod 8) D_i
-// for small-order ones), the torsion coefficients of the matching votes add (sum mod 8) T8.  Lanes
-// sum their votes' terms, the lanes that hold a term are compacted through LDS, and a shuffle tree
-// of ceil(log2(count)) levels adds them: the serial chain is a few point additions, not six levels
-// plus per-term multiples.
+// Exact sum of listed certificate c, by one wave (lane = 0..63; part: the wave's LDS rows): every
+// slow vote's record holds its term z_i D_i (k_slow_mul for prime-order components, k_slow_prep's
+// (z_i mod 8) D_i for small-order ones), the torsion coefficients of the matching votes add
+// (sum mod 8) T8.  Lanes sum their votes' terms, the lanes that hold a term are compacted through
+// LDS, and a shuffle tree of ceil(log2(count)) levels adds them: the serial chain is a few point
+// additions, not six levels plus per-term multiples.
+__device__ __forceinline__ void exact_cert(const FinalizeParams& a, uint32_t c, uint32_t lane, uint32_t (*part)[40]) {
+    const uint32_t first = a.cert_first[c], nv = a.cert_n[c];   // in range: bad ranges never get listed
+    ge_p3 acc = ge_to_vgpr(ge_identity());
+    bool has = false, bad = false;
+    uint32_t tsum = 0;
+    for (uint32_t v = lane; v < nv; v += 64) {
+        const uint32_t f = a.flags[first + v];
+        tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
+        if (f & NW_F_SLOW) {
+            const uint32_t* rec = a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS;
+            // a term must be final and this certificate's own (valid calls always satisfy both;
+            // a vote claimed by two certificates is NW_ERR_ARG and must not be accepted here)
+            const uint32_t kind = rec[SLOW_KIND];
+            if (a.sig_cert[first + v] != c || (kind != SK_SMALL && kind != SK_MUL)) {
+                bad = true;
+                continue;
+            }
+            const ge_p3 q = load_p3(rec);
+            acc = has ? ge_add(acc, ge_to_cached(q)) : q;
+            has = true;
+        }
+    }
+    bad = __any(bad);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) tsum += __shfl_xor(tsum, off, 64);
+    const uint32_t tk = tsum & 7u;
+    if (lane == 63 && tk != 0) {   // lane 63 adds (tk) T8 to its partial (binary: T8, 2 T8, 4 T8)
+        const ge_p3 t1 = ge_t8(), t2 = ge_dbl(t1), t4 = ge_dbl(t2);
+        ge_p3 t = ge_select(ge_identity(), t1, (tk & 1u) != 0);
+        t = ge_add(t, ge_to_cached(ge_select(ge_identity(), t2, (tk & 2u) != 0)));
+        t = ge_add(t, ge_to_cached(ge_select(ge_identity(), t4, (tk & 4u) != 0)));
+        acc = has ? ge_add(acc, ge_to_cached(t)) : t;
+        has = true;
+    }
+    const uint64_t mask = __ballot(has);
+    const uint32_t k = (uint32_t)__popcll(mask);
+    if (has) store_p3(part[__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))], acc);
+    __syncthreads();
+    acc = lane < k ? load_p3(part[lane]) : ge_identity();
+    __syncthreads();   // part is rewritten by the next listed certificate
+    for (uint32_t off = 1; off < k; off <<= 1) {   // k is wave-uniform
+        const ge_p3 o = ge_shfl_down(acc, off);
+        acc = ge_select(acc, ge_add(acc, ge_to_cached(o)), lane + off < k);
+    }
+    if (lane == 0 && a.cert_ok) a.cert_ok[c] = (!bad && ge_is_identity(acc)) ? 1 : 0;
+}
+
+// Per-certificate verdict: definitive Err on any bad S / undecodable A / undecodable R, else the
+// exact remaining batch sum (usually empty) must be the identity.  One wave per certificate: flag
+// reduction, stake sum, and the verdict whenever the flags decide it (parse / decode failure, all
+// votes matching, one term with a prime-order component).  The rest (two or more slow-path terms)
+// is appended to the exact list for k_cert_exact, which has the registers for the point sum: this
+// kernel stays at a handful of VGPRs and never spills.
+__global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t c = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (a.sig_ok) {   // strict verdict bytes of every signature (the flags are final here)
+        const uint32_t nthr = gridDim.x * blockDim.x;
+        for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < a.nsigs; v += nthr)
+            a.sig_ok[v] = (a.flags[v] & NW_F_STRICT) ? 1 : 0;
+    }
+    if (c >= a.ncerts) return;   // whole wave exits together
+    finalize_cert(a, c, lane);
+}
+
 static constexpr uint32_t EXACT_MAX_BLOCKS = 1024;
 __global__ void __launch_bounds__(64) k_cert_exact(FinalizeParams a) {
     __shared__ uint32_t part[64][40];
-    const uint32_t lane = threadIdx.x;
     const uint32_t cnt = *a.exact_count;
-    for (uint32_t e = blockIdx.x; e < cnt; e += gridDim.x) {
-        const uint32_t c = a.exact_list[e];
-        const uint32_t first = a.cert_first[c], nv = a.cert_n[c];   // in range: bad ranges never get listed
-        ge_p3 acc = ge_to_vgpr(ge_identity());
-        bool has = false, bad = false;
-        uint32_t tsum = 0;
-        for (uint32_t v = lane; v < nv; v += 64) {
-            const uint32_t f = a.flags[first + v];
-            tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
-            if (f & NW_F_SLOW) {
-                const uint32_t* rec = a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS;
-                // a term must be final and this certificate's own (valid calls always satisfy both;
-                // a vote claimed by two certificates is NW_ERR_ARG and must not be accepted here)
-                const uint32_t kind = rec[SLOW_KIND];
-                if (a.sig_cert[first + v] != c || (kind != SK_SMALL && kind != SK_MUL)) {
-                    bad = true;
-                    continue;
-                }
-                const ge_p3 q = load_p3(rec);
-                acc = has ? ge_add(acc, ge_to_cached(q)) : q;
-                has = true;
-            }
-        }
-        bad = __any(bad);
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) tsum += __shfl_xor(tsum, off, 64);
-        const uint32_t tk = tsum & 7u;
-        if (lane == 63 && tk != 0) {   // lane 63 adds (tk) T8 to its partial (binary: T8, 2 T8, 4 T8)
-            const ge_p3 t1 = ge_t8(), t2 = ge_dbl(t1), t4 = ge_dbl(t2);
-            ge_p3 t = ge_select(ge_identity(), t1, (tk & 1u) != 0);
-            t = ge_add(t, ge_to_cached(ge_select(ge_identity(), t2, (tk & 2u) != 0)));
-            t = ge_add(t, ge_to_cached(ge_select(ge_identity(), t4, (tk & 4u) != 0)));
-            acc = has ? ge_add(acc, ge_to_cached(t)) : t;
-            has = true;
-        }
-        const uint64_t mask = __ballot(has);
-        const uint32_t k = (uint32_t)__popcll(mask);
-        if (has) store_p3(part[__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))], acc);
-        __syncthreads();
-        acc = lane < k ? load_p3(part[lane]) : ge_identity();
-        __syncthreads();   // part is rewritten by the next listed certificate
-        for (uint32_t off = 1; off < k; off <<= 1) {   // k is wave-uniform
-            const ge_p3 o = ge_shfl_down(acc, off);
-            acc = ge_select(acc, ge_add(acc, ge_to_cached(o)), lane + off < k);
-        }
-        if (lane == 0 && a.cert_ok) a.cert_ok[c] = (!bad && ge_is_identity(acc)) ? 1 : 0;
-    }
+    for (uint32_t e = blockIdx.x; e < cnt; e += gridDim.x) exact_cert(a, a.exact_list[e], threadIdx.x, part);
+}
+
+// Both in one wave for calls of a few certificates (a single certificate, header batch or vote
+// batch): one launch instead of two (~5 us each even when the exact list is empty).  The wave reads
+// back the exact list its own lanes appended: a device-scope fence and atomic reads order them.
+static constexpr uint32_t TAIL_MAX_CERTS = 16;
+__global__ void __launch_bounds__(64) k_cert_tail(FinalizeParams a) {
+    __shared__ uint32_t part[64][40];
+    const uint32_t lane = threadIdx.x;
+    if (a.sig_ok)
+        for (uint32_t v = lane; v < a.nsigs; v += 64) a.sig_ok[v] = (a.flags[v] & NW_F_STRICT) ? 1 : 0;
+    for (uint32_t c = 0; c < a.ncerts; ++c) finalize_cert(a, c, lane);
+    __threadfence();
+    __syncthreads();
+    const uint32_t cnt = __hip_atomic_load(a.exact_count, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t e = 0; e < cnt; ++e)
+        exact_cert(a, __hip_atomic_load(a.exact_list + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), lane, part);
 }
 
 // ------------------------------------------------------------------------------------ batch preamble
@@ -495,6 +523,10 @@ hipError_t launch_finish(const VerifyParams& p, hipStream_t st) {
 
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
     if (p.ncerts == 0) return hipSuccess;
+    if (p.ncerts <= TAIL_MAX_CERTS && p.nsigs <= 64u * 1024u) {
+        hipLaunchKernelGGL(k_cert_tail, dim3(1), dim3(64), 0, st, p);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(k_cert_finalize, dim3(blocks_for((uint64_t)p.ncerts * 64, 256)), dim3(256), 0, st, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

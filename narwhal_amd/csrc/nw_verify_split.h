@@ -143,10 +143,12 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
         P = ge_add(P, ge_to_cached(o));
     }
     if constexpr (FUSE) {
-        const uint32_t pf = park_mismatch(a, i, P, verify_pflags(P, R, flags));
+        const bool emits = j == 0 && owner;   // the group's writer (the other lanes: same chain, no stores)
+        uint32_t pf = verify_pflags(P, R, flags);
+        if (emits) pf = park_mismatch(a, i, P, pf);
         const fe zi = (NW_INV_VAR && a.gn <= 8) ? fe_invert_var(P.Z) : fe_invert_sg(P.Z);
         const uint32_t f = finish_x_flags(P.X, zi, pf);
-        if (j == 0 && owner) finish_emit(a, i, pf, f);
+        if (emits) finish_emit(a, i, pf, f);
         return;
     }
     if (j != 0 || !owner) return;
