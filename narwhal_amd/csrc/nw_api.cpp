@@ -735,8 +735,6 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     if (!split_fuses_finish(vp.gn, vp.fk)) NW_TRY(launch_finish(vp, st), "k_finish");
     if (!batch_mode) return NW_OK;   // strict verdicts only (bytes written by k_finish): no certificate pass
 
-    NW_TRY(launch_slow(vp, msgmode, ctx->key_window, (uint32_t)nsigs, st), "k_slow_prep / k_slow_mul");
-
     FinalizeParams fp{};
     fp.ncerts = (uint32_t)ncerts;
     fp.nsigs = (uint32_t)nsigs;
@@ -754,6 +752,11 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     fp.sig_ok = d_sig_ok;
     fp.exact_count = slow_count + 1;   // word 1 of the zeroed slow-path counter block
     fp.exact_list = ws->w_exact.as<uint32_t>();
+    if (slow_tail_fits(ncerts, nsigs)) {   // one header / vote batch: exact path + finalize in one launch
+        NW_TRY(launch_slow_tail(vp, fp, msgmode, ctx->key_window, st), "k_slow_tail");
+        return NW_OK;
+    }
+    NW_TRY(launch_slow(vp, msgmode, ctx->key_window, (uint32_t)nsigs, st), "k_slow_prep / k_slow_mul");
     NW_TRY(launch_finalize(fp, st), "k_cert_finalize / k_cert_exact");
     return NW_OK;
 }

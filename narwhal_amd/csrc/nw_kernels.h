@@ -111,6 +111,15 @@ hipError_t launch_finish(const VerifyParams& p, hipStream_t st);
 // entries); both read the device slow counter, so honest batches find no work.
 hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint32_t n_upper, hipStream_t st);
 hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st);
+// Calls of at most TAIL_MAX_CERTS certificates finalize in one wave (k_cert_tail); with at most
+// SLOW_TAIL_MAX_SIGS signatures as well, the whole exact path and the finalize run in one workgroup
+// (k_slow_tail, launch_slow_tail) instead of launch_slow + launch_finalize.
+static constexpr uint32_t TAIL_MAX_CERTS = 16;
+static constexpr uint32_t SLOW_TAIL_MAX_SIGS = 256;
+inline bool slow_tail_fits(uint64_t ncerts, uint64_t nsigs) {
+    return ncerts >= 1 && ncerts <= TAIL_MAX_CERTS && nsigs >= 1 && nsigs <= SLOW_TAIL_MAX_SIGS;
+}
+hipError_t launch_slow_tail(const VerifyParams& p, const FinalizeParams& f, int msgmode, int key_window, hipStream_t st);
 // Batch preamble: reset sig_cert to NO_CERT, zero counts (may be null: no histogram) / the slow
 // counter / status (may be null: no input check), expand certificates (a vote claimed by two
 // certificates is NW_ERR_ARG), histogram + check signer slots (k_prep_certs, k_expand_count); then

@@ -16,6 +16,8 @@
 // Pipeline per batch: k_prep_certs + k_expand_count -> [signer grouping] -> k_verify (P_i, one lane per signature)
 // -> k_finish (Montgomery batch inversion of Z over FINISH_K signatures per lane, encoding match,
 // strict verdict) -> k_slow_prep / k_slow_mul (compacted list of mismatches only) -> k_cert_finalize.
+// Small calls (<= 16 certificates, <= 256 signatures) run everything after k_verify_split's fused finish
+// as one workgroup: k_slow_tail (nw_verify_kernels.h).
 #include <hip/hip_runtime.h>
 #include <algorithm>
 #include <cstdlib>
@@ -24,6 +26,8 @@
 #include "nw_kernels.h"
 #include "nw_core.h"
 #include "nw_quad.h"
+#include "nw_cert.h"
+#include "nw_verify_kernels.h"
 
 namespace nw {
 
@@ -35,6 +39,12 @@ extern template hipError_t launch_vs_wa<12>(const VerifyParams&, int, bool, uint
 extern template hipError_t launch_vs_wa<13>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
 extern template hipError_t launch_vs_wa<16>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
 extern template hipError_t launch_vs_wa<20>(const VerifyParams&, int, bool, uint32_t, hipStream_t);
+extern template hipError_t launch_slow_tail_wa<8>(const VerifyParams&, const FinalizeParams&, int, hipStream_t);
+extern template hipError_t launch_slow_tail_wa<9>(const VerifyParams&, const FinalizeParams&, int, hipStream_t);
+extern template hipError_t launch_slow_tail_wa<12>(const VerifyParams&, const FinalizeParams&, int, hipStream_t);
+extern template hipError_t launch_slow_tail_wa<13>(const VerifyParams&, const FinalizeParams&, int, hipStream_t);
+extern template hipError_t launch_slow_tail_wa<16>(const VerifyParams&, const FinalizeParams&, int, hipStream_t);
+extern template hipError_t launch_slow_tail_wa<20>(const VerifyParams&, const FinalizeParams&, int, hipStream_t);
 
 // ------------------------------------------------------------------------------------ signer grouping
 // Counting sort of signature indices by key-cache slot: perm lists the signatures of slot 0, then
@@ -179,112 +189,6 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
 }
 
 // Per-certificate verdict: definitive Err on any bad S / undecodable A / undecodable R, else the
-// exact remaining batch sum (usually empty) must be the identity.  One 64-lane wave per
-// certificate: lanes stride over the votes (coalesced flag reads), wave reductions combine them;
-// the exact sum over slow-path terms (failing certificates only) is a lane-strided sum + shuffle tree.
-// One wave per certificate: flag reduction, stake sum, and the verdict whenever the flags decide it
-// (parse / decode failure, all votes matching, one term with a prime-order component).  The rest
-// (two or more slow-path terms) is appended to the exact list for k_cert_exact, which has the
-// registers for the point sum: this kernel stays at a handful of VGPRs and never spills.
-// Certificate c's finalize, by one wave (lane = 0..63).
-__device__ __forceinline__ void finalize_cert(const FinalizeParams& a, uint32_t c, uint32_t lane) {
-    const uint32_t first = a.cert_first[c];
-    // a vote range past the signature array (device inputs are not host-checked) rejects the
-    // certificate; only the in-range votes are read
-    const bool range_bad = (uint64_t)first + a.cert_n[c] > a.nsigs;
-    const uint32_t nv = range_bad ? (first < a.nsigs ? a.nsigs - first : 0u) : a.cert_n[c];
-    // CS_DOOM: a bad S / undecodable A (the flags say so too) or a vote range overlapping another
-    // certificate's (k_expand_count)
-    bool bad = range_bad || (a.cert_state && (a.cert_state[c] & CS_DOOM)), slow = false;
-    uint32_t tsum = 0;
-    uint64_t stake = 0;
-    for (uint32_t v = lane; v < nv; v += 64) {
-        const uint32_t f = a.flags[first + v];
-        // a vote this certificate does not own (overlapping device ranges, NW_ERR_ARG) was checked
-        // against its owner's message: it rejects this certificate and adds none of its stake
-        const bool own = a.sig_cert[first + v] == c;
-        bad = bad || !own || ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) || (f & NW_F_R_BAD);
-        slow = slow || (f & NW_F_SLOW);
-        tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
-        if (own && (f & NW_F_STRICT)) stake += a.stake[a.signer[first + v]];
-    }
-    bad = __any(bad);
-    slow = __any(slow);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        tsum += __shfl_xor(tsum, off, 64);
-        stake += __shfl_xor(stake, off, 64);
-    }
-    if (lane != 0) return;
-    if (a.accepted_stake) a.accepted_stake[c] = stake;
-    bool ok;
-    if (bad) {
-        ok = false;
-    } else if (!slow) {
-        ok = (tsum & 7u) == 0;
-    } else if ((a.cert_state[c] & CS_BIG_MASK) == 1u) {
-        ok = false;   // one term with a prime-order component: the sum cannot be the identity (k_slow_prep)
-    } else {
-        a.exact_list[atomicAdd(a.exact_count, 1u)] = c;   // the exact sum writes the verdict
-        return;
-    }
-    if (a.cert_ok) a.cert_ok[c] = ok ? 1 : 0;
-}
-
-// Exact sum of listed certificate c, by one wave (lane = 0..63; part: the wave's LDS rows): every
-// slow vote's record holds its term z_i D_i (k_slow_mul for prime-order components, k_slow_prep's
-// (z_i mod 8) D_i for small-order ones), the torsion coefficients of the matching votes add
-// (sum mod 8) T8.  Lanes sum their votes' terms, the lanes that hold a term are compacted through
-// LDS, and a shuffle tree of ceil(log2(count)) levels adds them: the serial chain is a few point
-// additions, not six levels plus per-term multiples.
-__device__ __forceinline__ void exact_cert(const FinalizeParams& a, uint32_t c, uint32_t lane, uint32_t (*part)[40]) {
-    const uint32_t first = a.cert_first[c], nv = a.cert_n[c];   // in range: bad ranges never get listed
-    ge_p3 acc = ge_to_vgpr(ge_identity());
-    bool has = false, bad = false;
-    uint32_t tsum = 0;
-    for (uint32_t v = lane; v < nv; v += 64) {
-        const uint32_t f = a.flags[first + v];
-        tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
-        if (f & NW_F_SLOW) {
-            const uint32_t* rec = a.slow_buf + (size_t)a.slow_slot[first + v] * SLOW_WORDS;
-            // a term must be final and this certificate's own (valid calls always satisfy both;
-            // a vote claimed by two certificates is NW_ERR_ARG and must not be accepted here)
-            const uint32_t kind = rec[SLOW_KIND];
-            if (a.sig_cert[first + v] != c || (kind != SK_SMALL && kind != SK_MUL)) {
-                bad = true;
-                continue;
-            }
-            const ge_p3 q = load_p3(rec);
-            acc = has ? ge_add(acc, ge_to_cached(q)) : q;
-            has = true;
-        }
-    }
-    bad = __any(bad);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) tsum += __shfl_xor(tsum, off, 64);
-    const uint32_t tk = tsum & 7u;
-    if (lane == 63 && tk != 0) {   // lane 63 adds (tk) T8 to its partial (binary: T8, 2 T8, 4 T8)
-        const ge_p3 t1 = ge_t8(), t2 = ge_dbl(t1), t4 = ge_dbl(t2);
-        ge_p3 t = ge_select(ge_identity(), t1, (tk & 1u) != 0);
-        t = ge_add(t, ge_to_cached(ge_select(ge_identity(), t2, (tk & 2u) != 0)));
-        t = ge_add(t, ge_to_cached(ge_select(ge_identity(), t4, (tk & 4u) != 0)));
-        acc = has ? ge_add(acc, ge_to_cached(t)) : t;
-        has = true;
-    }
-    const uint64_t mask = __ballot(has);
-    const uint32_t k = (uint32_t)__popcll(mask);
-    if (has) store_p3(part[__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))], acc);
-    __syncthreads();
-    acc = lane < k ? load_p3(part[lane]) : ge_identity();
-    __syncthreads();   // part is rewritten by the next listed certificate
-    for (uint32_t off = 1; off < k; off <<= 1) {   // k is wave-uniform
-        const ge_p3 o = ge_shfl_down(acc, off);
-        acc = ge_select(acc, ge_add(acc, ge_to_cached(o)), lane + off < k);
-    }
-    if (lane == 0 && a.cert_ok) a.cert_ok[c] = (!bad && ge_is_identity(acc)) ? 1 : 0;
-}
-
-// Per-certificate verdict: definitive Err on any bad S / undecodable A / undecodable R, else the
 // exact remaining batch sum (usually empty) must be the identity.  One wave per certificate: flag
 // reduction, stake sum, and the verdict whenever the flags decide it (parse / decode failure, all
 // votes matching, one term with a prime-order component).  The rest (two or more slow-path terms)
@@ -312,18 +216,9 @@ __global__ void __launch_bounds__(64) k_cert_exact(FinalizeParams a) {
 // Both in one wave for calls of a few certificates (a single certificate, header batch or vote
 // batch): one launch instead of two (~5 us each even when the exact list is empty).  The wave reads
 // back the exact list its own lanes appended: a device-scope fence and atomic reads order them.
-static constexpr uint32_t TAIL_MAX_CERTS = 16;
 __global__ void __launch_bounds__(64) k_cert_tail(FinalizeParams a) {
     __shared__ uint32_t part[64][40];
-    const uint32_t lane = threadIdx.x;
-    if (a.sig_ok)
-        for (uint32_t v = lane; v < a.nsigs; v += 64) a.sig_ok[v] = (a.flags[v] & NW_F_STRICT) ? 1 : 0;
-    for (uint32_t c = 0; c < a.ncerts; ++c) finalize_cert(a, c, lane);
-    __threadfence();
-    __syncthreads();
-    const uint32_t cnt = __hip_atomic_load(a.exact_count, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t e = 0; e < cnt; ++e)
-        exact_cert(a, __hip_atomic_load(a.exact_list + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), lane, part);
+    cert_tail(a, threadIdx.x, part);
 }
 
 // ------------------------------------------------------------------------------------ batch preamble
@@ -409,79 +304,10 @@ __global__ void __launch_bounds__(256) k_flags_to_ok(uint32_t n, const uint32_t*
     if (i < n) ok[i] = (flags[i] & NW_F_STRICT) ? 1 : 0;
 }
 
-// ------------------------------------------------------------------------------------ exact path, step 2
-// z_i D_i for the SK_BIG entries of certificates that have two or more of them (the only case the
-// direct-sum argument of k_slow_prep cannot decide): one quad per entry, every point operation
-// split over the quad's 4 lanes (nw_quad.h), signed radix-16 digits of the 128-bit z_i with the
-// multiples 1..8 D_i in LDS: 7 table operations + 128 doublings + 32 additions on the quad.
-// 256-thread workgroups (64 quads) with the entries dealt to the blocks first: an adversarial
-// batch's few hundred entries land on wave 0 of every block, one working wave per CU (one-wave
-// blocks were packed up to three to a SIMD by the dispatcher, stretching the serial chains).
-static constexpr uint32_t SLOW_MUL_QUADS = 64;   // per 256-thread workgroup
+// Exact path, step 2 (slow_mul in nw_verify_kernels.h) over up to 256 workgroups.
 __global__ void __launch_bounds__(256) k_slow_mul(VerifyParams a) {
     __shared__ uint32_t tab[SLOW_MUL_QUADS][8][40];
-    const uint32_t cnt = *a.slow_count;
-    const uint32_t qd = threadIdx.x >> 2, q = threadIdx.x & 3u;
-    uint32_t (*T)[40] = tab[qd];
-    // entries dealt to the blocks first (one wave each), as in k_slow_prep: a wave's time is one
-    // chain whatever its number of quads, so spreading the entries keeps the waves short and apart.
-    // A wave with fewer entries than quads runs duplicate chains of its own entries on the idle
-    // quads (own LDS table slot, no record writes), so its EXEC mask stays full.
-    const uint32_t wq = (threadIdx.x & 63u) >> 2;                    // quad index inside the wave
-    for (uint32_t base = (qd - wq) * gridDim.x + blockIdx.x; base < cnt; base += gridDim.x * SLOW_MUL_QUADS) {
-        const uint32_t t_own = base + wq * gridDim.x;
-        const uint32_t v = (uint32_t)__popcll(__ballot(t_own < cnt)) >> 2;   // entries of this wave: quads [0, v)
-        const bool owner = wq < v;
-        const uint32_t t = owner ? t_own : base + (wq % v) * gridDim.x;
-        uint32_t* rec = a.slow_buf + (size_t)t * SLOW_WORDS;
-        if (rec[SLOW_KIND] != SK_BIG) continue;                      // uniform over the quad
-        const uint32_t i = a.slow_list[t];
-        const uint32_t cert = a.sig_cert[i];
-        const uint32_t cs = a.cert_state[cert];
-        if ((cs & (CS_DOOM | CS_RDOOM)) || (cs & CS_BIG_MASK) < 2u) continue;
-        const ge_p3 D = ge_to_vgpr(load_p3(rec));
-        uint32_t z4[4];
-        coeff_z(a, i, cert, z4);
-        // T[k] = (k + 1) D
-        ge_p3 m = D;
-        if (q == 0) store_p3(T[0], m);
-        m = ge_dbl_quad(D);
-        if (q == 0) store_p3(T[1], m);
-#pragma nounroll
-        for (int k = 2; k < 8; ++k) {
-            m = ge_add_quad(m, D);
-            if (q == 0) store_p3(T[k], m);
-        }
-        __builtin_amdgcn_wave_barrier();
-        // signed radix-16 digits d_0..d_31 in [-8, 8) plus a top carry d_32 in {0, 1}, packed as
-        // nibbles with d_31 in the top nibble so the Horner loop shifts them out from the top
-        uint32_t pk[4] = {0u, 0u, 0u, 0u};
-        uint32_t carry = 0;
-#pragma unroll
-        for (int j = 0; j < 32; ++j) {
-            const uint32_t b = ((z4[j >> 3] >> (4 * (j & 7))) & 15u) + carry;
-            carry = b >= 8u ? 1u : 0u;
-            pk[j >> 3] |= ((b - 16u * carry) & 15u) << (4 * (j & 7));
-        }
-        ge_p3 acc = ge_select(ge_to_vgpr(ge_identity()), D, carry != 0);
-#pragma nounroll
-        for (int j = 31; j >= 0; --j) {
-            acc = ge_dbl_quad(ge_dbl_quad(ge_dbl_quad(ge_dbl_quad(acc))));
-            const int d = (int)(pk[3] << 0) >> 28;                  // top nibble, sign-extended
-#pragma unroll
-            for (int w = 3; w > 0; --w) pk[w] = (pk[w] << 4) | (pk[w - 1] >> 28);
-            pk[0] <<= 4;
-            if (d != 0) {
-                const ge_p3 e = load_p3(T[(d < 0 ? -d : d) - 1]);
-                acc = ge_add_quad(acc, d < 0 ? ge_neg(e) : e);
-            }
-        }
-        if (q == 0 && owner) {
-            store_p3(rec, acc);
-            rec[SLOW_KIND] = SK_MUL;
-        }
-        __builtin_amdgcn_wave_barrier();   // the table slot is rewritten by this quad's next entry
-    }
+    slow_mul(a, blockIdx.x, gridDim.x, tab);
 }
 
 // ------------------------------------------------------------------------------------ launchers
@@ -510,6 +336,19 @@ hipError_t launch_slow(const VerifyParams& p, int msgmode, int key_window, uint3
     const uint32_t nb = std::min<uint32_t>(blocks_for(n_upper, SLOW_MUL_QUADS), 256u);
     hipLaunchKernelGGL(k_slow_mul, dim3(nb), dim3(256), 0, st, p);
     return hipGetLastError();
+}
+
+hipError_t launch_slow_tail(const VerifyParams& p, const FinalizeParams& f, int msgmode, int key_window,
+                            hipStream_t st) {
+    switch (key_window) {
+        case 8: return launch_slow_tail_wa<8>(p, f, msgmode, st);
+        case 9: return launch_slow_tail_wa<9>(p, f, msgmode, st);
+        case 12: return launch_slow_tail_wa<12>(p, f, msgmode, st);
+        case 13: return launch_slow_tail_wa<13>(p, f, msgmode, st);
+        case 16: return launch_slow_tail_wa<16>(p, f, msgmode, st);
+        case 20: return launch_slow_tail_wa<20>(p, f, msgmode, st);
+        default: return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_finish(const VerifyParams& p, hipStream_t st) {

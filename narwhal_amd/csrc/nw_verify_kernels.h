@@ -8,6 +8,8 @@
 #include "nw_chacha.h"
 #include "nw_kernels.h"
 #include "nw_core.h"
+#include "nw_quad.h"
+#include "nw_cert.h"
 
 namespace nw {
 
@@ -137,8 +139,9 @@ hipError_t launch_split_wa(const VerifyParams& p, int msgmode, hipStream_t st);
 // identity (its prime-order component is z_i D_i' != O) and is rejected without any scalar
 // multiplication; only certificates with two or more SK_BIG entries need z_i D_i (k_slow_mul).
 // Entries of certificates already rejected (bad S / undecodable A, from k_finish) are skipped.
+// (bid, nb): this workgroup's index among the nb workgroups that share the list.
 template <int MSGMODE, int WA>
-__global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
+__device__ __forceinline__ void slow_prep(const VerifyParams& a, uint32_t bid, uint32_t nb) {
 #ifdef NW_SLOW_TIMING
     const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -150,13 +153,13 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
     // measured at C5 with per-entry timestamps).  A wave with fewer entries than lanes runs
     // duplicate chains of its own entries on the idle lanes (no writes): a wave with a sparse EXEC
     // mask issues its chain up to 1.8x slower on some CUs.
-    const uint32_t nthr = gridDim.x * blockDim.x;
+    const uint32_t nthr = nb * blockDim.x;
     const uint32_t lane = threadIdx.x & 63u;
-    for (uint32_t base = (threadIdx.x - lane) * gridDim.x + blockIdx.x; base < cnt; base += nthr) {   // wave-uniform
-        const uint32_t t_own = base + lane * gridDim.x;
+    for (uint32_t base = (threadIdx.x - lane) * nb + bid; base < cnt; base += nthr) {   // wave-uniform
+        const uint32_t t_own = base + lane * nb;
         const uint32_t v = (uint32_t)__popcll(__ballot(t_own < cnt));   // entries of this wave: lanes [0, v)
         const bool owner = lane < v;
-        const uint32_t t = owner ? t_own : base + (lane % v) * gridDim.x;
+        const uint32_t t = owner ? t_own : base + (lane % v) * nb;
         const uint32_t i = a.slow_list[t];
         uint32_t* rec = a.slow_buf + (size_t)t * SLOW_WORDS;
         const uint32_t cert = a.sig_cert[i];   // slow-list entries always have an owner (k_finish)
@@ -226,6 +229,103 @@ __global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
     }
 }
 
+template <int MSGMODE, int WA>
+__global__ void __launch_bounds__(256) k_slow_prep(VerifyParams a) {
+    slow_prep<MSGMODE, WA>(a, blockIdx.x, gridDim.x);
+}
+
+// ------------------------------------------------------------------------------------ exact path, step 2
+// z_i D_i for the SK_BIG entries of certificates that have two or more of them (the only case the
+// direct-sum argument of k_slow_prep cannot decide): one quad per entry, every point operation
+// split over the quad's 4 lanes (nw_quad.h), signed radix-16 digits of the 128-bit z_i with the
+// multiples 1..8 D_i in LDS: 7 table operations + 128 doublings + 32 additions on the quad.
+// 256-thread workgroups (64 quads) with the entries dealt to the blocks first: an adversarial
+// batch's few hundred entries land on wave 0 of every block, one working wave per CU (one-wave
+// blocks were packed up to three to a SIMD by the dispatcher, stretching the serial chains).
+static constexpr uint32_t SLOW_MUL_QUADS = 64;   // per 256-thread workgroup
+__device__ __forceinline__ void slow_mul(const VerifyParams& a, uint32_t bid, uint32_t nb, uint32_t (*tab)[8][40]) {
+    const uint32_t cnt = *a.slow_count;
+    const uint32_t qd = threadIdx.x >> 2, q = threadIdx.x & 3u;
+    uint32_t (*T)[40] = tab[qd];
+    // entries dealt to the blocks first (one wave each), as in k_slow_prep: a wave's time is one
+    // chain whatever its number of quads, so spreading the entries keeps the waves short and apart.
+    // A wave with fewer entries than quads runs duplicate chains of its own entries on the idle
+    // quads (own LDS table slot, no record writes), so its EXEC mask stays full.
+    const uint32_t wq = (threadIdx.x & 63u) >> 2;                    // quad index inside the wave
+    for (uint32_t base = (qd - wq) * nb + bid; base < cnt; base += nb * SLOW_MUL_QUADS) {
+        const uint32_t t_own = base + wq * nb;
+        const uint32_t v = (uint32_t)__popcll(__ballot(t_own < cnt)) >> 2;   // entries of this wave: quads [0, v)
+        const bool owner = wq < v;
+        const uint32_t t = owner ? t_own : base + (wq % v) * nb;
+        uint32_t* rec = a.slow_buf + (size_t)t * SLOW_WORDS;
+        if (rec[SLOW_KIND] != SK_BIG) continue;                      // uniform over the quad
+        const uint32_t i = a.slow_list[t];
+        const uint32_t cert = a.sig_cert[i];
+        const uint32_t cs = a.cert_state[cert];
+        if ((cs & (CS_DOOM | CS_RDOOM)) || (cs & CS_BIG_MASK) < 2u) continue;
+        const ge_p3 D = ge_to_vgpr(load_p3(rec));
+        uint32_t z4[4];
+        coeff_z(a, i, cert, z4);
+        // T[k] = (k + 1) D
+        ge_p3 m = D;
+        if (q == 0) store_p3(T[0], m);
+        m = ge_dbl_quad(D);
+        if (q == 0) store_p3(T[1], m);
+#pragma nounroll
+        for (int k = 2; k < 8; ++k) {
+            m = ge_add_quad(m, D);
+            if (q == 0) store_p3(T[k], m);
+        }
+        __builtin_amdgcn_wave_barrier();
+        // signed radix-16 digits d_0..d_31 in [-8, 8) plus a top carry d_32 in {0, 1}, packed as
+        // nibbles with d_31 in the top nibble so the Horner loop shifts them out from the top
+        uint32_t pk[4] = {0u, 0u, 0u, 0u};
+        uint32_t carry = 0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const uint32_t b = ((z4[j >> 3] >> (4 * (j & 7))) & 15u) + carry;
+            carry = b >= 8u ? 1u : 0u;
+            pk[j >> 3] |= ((b - 16u * carry) & 15u) << (4 * (j & 7));
+        }
+        ge_p3 acc = ge_select(ge_to_vgpr(ge_identity()), D, carry != 0);
+#pragma nounroll
+        for (int j = 31; j >= 0; --j) {
+            acc = ge_dbl_quad(ge_dbl_quad(ge_dbl_quad(ge_dbl_quad(acc))));
+            const int d = (int)(pk[3] << 0) >> 28;                  // top nibble, sign-extended
+#pragma unroll
+            for (int w = 3; w > 0; --w) pk[w] = (pk[w] << 4) | (pk[w - 1] >> 28);
+            pk[0] <<= 4;
+            if (d != 0) {
+                const ge_p3 e = load_p3(T[(d < 0 ? -d : d) - 1]);
+                acc = ge_add_quad(acc, d < 0 ? ge_neg(e) : e);
+            }
+        }
+        if (q == 0 && owner) {
+            store_p3(rec, acc);
+            rec[SLOW_KIND] = SK_MUL;
+        }
+        __builtin_amdgcn_wave_barrier();   // the table slot is rewritten by this quad's next entry
+    }
+}
+
+// The whole exact path of a small call (at most SLOW_TAIL_MAX_SIGS signatures and TAIL_MAX_CERTS
+// certificates: one header, one vote batch) in ONE workgroup: k_slow_prep, k_slow_mul and
+// k_cert_tail as three phases with a workgroup barrier between them, one launch instead of three
+// (~4-5 us of dispatch each, the whole cost when the slow list is empty).  Phase 1 gives every
+// entry a lane of its own (256 >= nsigs); phase 2 runs 64 quads per pass; phase 3 is wave 0's.
+template <int MSGMODE, int WA>
+__global__ void __launch_bounds__(256) k_slow_tail(VerifyParams a, FinalizeParams f) {
+    __shared__ uint32_t tab[SLOW_MUL_QUADS][8][40];
+    slow_prep<MSGMODE, WA>(a, 0u, 1u);
+    __threadfence();
+    __syncthreads();
+    slow_mul(a, 0u, 1u, tab);
+    __threadfence();
+    __syncthreads();   // tab is free again: phase 3 reuses it for its partial sums
+    if (threadIdx.x >= 64) return;
+    cert_tail(f, threadIdx.x, reinterpret_cast<uint32_t (*)[40]>(&tab[0][0][0]));
+}
+
 // Launch k_verify (slow = false, grid over p.gn) or k_slow_prep (slow = true: a grid-stride grid
 // capped at one 256-thread block per CU, so an honest batch's empty exact path costs one small
 // dispatch whatever n_upper is).
@@ -246,6 +346,14 @@ hipError_t launch_vs_wa(const VerifyParams& p, int msgmode, bool slow, uint32_t 
         else if (p.key_negtab) hipLaunchKernelGGL((k_verify<1, WA, true>), g, b, 0, st, p);
         else hipLaunchKernelGGL((k_verify<1, WA, false>), g, b, 0, st, p);
     }
+    return hipGetLastError();
+}
+
+template <int WA>
+hipError_t launch_slow_tail_wa(const VerifyParams& p, const FinalizeParams& f, int msgmode, hipStream_t st) {
+    if (!slow_tail_fits(f.ncerts, f.nsigs)) return hipErrorInvalidValue;
+    if (msgmode == 0) hipLaunchKernelGGL((k_slow_tail<0, WA>), dim3(1), dim3(256), 0, st, p, f);
+    else hipLaunchKernelGGL((k_slow_tail<1, WA>), dim3(1), dim3(256), 0, st, p, f);
     return hipGetLastError();
 }
 
