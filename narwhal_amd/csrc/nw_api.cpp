@@ -899,8 +899,22 @@ size_t message_stage_bytes(size_t total, size_t n) { return align256(total + 8) 
 
 // Pack per-signature messages into the workspace (MSGMODE 1).
 int upload_messages(nw_ctx* ctx, Workspace* ws, Stager& sg, const uint8_t* const* msg, const size_t* len, size_t n,
-                    size_t total) {
+                    size_t total, uint64_t* fixed_len = nullptr) {
     NW_TRY(ws->ensure(ws->w_msg, total + 8), "ws msg");
+    if (fixed_len) {
+        // messages of one length laid out back to back (the worker's 8-byte messages, numpy rows):
+        // one block, no offset / length arrays (*fixed_len = the length; UINT64_MAX otherwise)
+        bool ok = n > 0;
+        for (size_t i = 1; ok && i < n; ++i) ok = len[i] == len[0] && msg[i] == msg[0] + i * len[0];
+        *fixed_len = ok ? (uint64_t)len[0] : UINT64_MAX;
+        if (ok) {
+            uint8_t* packed = sg.alloc(total + 8);
+            if (total) std::memcpy(packed, msg[0], total);
+            std::memset(packed + total, 0, 8);
+            NW_TRY(sg.copy(ws->w_msg.p, packed, total + 8), "H2D msg");
+            return NW_OK;
+        }
+    }
     NW_TRY(ws->ensure(ws->w_msg_off, n * 8 + 8), "ws msg_off");
     NW_TRY(ws->ensure(ws->w_msg_len, n * 8 + 8), "ws msg_len");
     uint8_t* packed = sg.alloc(total + 8);
@@ -966,7 +980,7 @@ int enqueue_strict_var(nw_ctx* ctx, Workspace* ws, size_t n, hipStream_t st, uin
 // bad_out (device, [nb] u32) receives the parse/decode failure flags.
 int enqueue_msm(nw_ctx* ctx, Workspace* ws, size_t nb, const uint32_t* counts, size_t nsig, const uint8_t* zseed,
                 uint64_t batch_base, uint32_t z_off, uint8_t* d_batch_ok, uint32_t* d_point_out, uint32_t** d_bad_out,
-                hipStream_t st) {
+                hipStream_t st, uint64_t msg_flen) {
     uint32_t nmax = 0;
     for (size_t b = 0; b < nb; ++b) nmax = counts[b] > nmax ? counts[b] : nmax;
     const uint32_t C = nmax >= 512 ? 8 : 7;
@@ -1025,6 +1039,7 @@ int enqueue_msm(nw_ctx* ctx, Workspace* ws, size_t nb, const uint32_t* counts, s
     mp.msg_base = ws->w_msg.as<uint8_t>();
     mp.msg_off = ws->w_msg_off.as<uint64_t>();
     mp.msg_len = ws->w_msg_len.as<uint64_t>();
+    mp.msg_flen = msg_flen;
     mp.batch_base = batch_base;
     mp.z_off = z_off;
     std::memcpy(mp.zseed, zseed, 32);
@@ -1038,6 +1053,9 @@ int enqueue_msm(nw_ctx* ctx, Workspace* ws, size_t nb, const uint32_t* counts, s
     mp.part = ws->w_msm_part.as<uint32_t>();
     mp.wpart = ws->w_msm_wpart.as<uint32_t>();
     mp.wfirst = reinterpret_cast<const uint32_t*>(dm + o_wf);
+    mp.one_task_windows = 1;
+    for (size_t k = 0; k < nb * NA; ++k)
+        if (wfirst[k + 1] - wfirst[k] != 1u || wfirst[k] != k) mp.one_task_windows = 0;
     mp.btab = ctx->d_btab;
     mp.batch_ok = d_batch_ok;
     mp.point_out = d_point_out;
@@ -1047,12 +1065,14 @@ int enqueue_msm(nw_ctx* ctx, Workspace* ws, size_t nb, const uint32_t* counts, s
 }
 
 // Upload per-signature messages, signatures and raw keys to the workspace (uncached-key paths).
+// fixed_len (MSM callers, whose kernel reads either form): see upload_messages.
 int upload_sig_keys(nw_ctx* ctx, Workspace* ws, const uint8_t* const* msg, const size_t* len,
-                    const uint8_t (*pk)[32], const uint8_t (*sig)[64], size_t n, hipStream_t st) {
+                    const uint8_t (*pk)[32], const uint8_t (*sig)[64], size_t n, hipStream_t st,
+                    uint64_t* fixed_len = nullptr) {
     const size_t total = message_bytes(len, n);
     Stager sg(ws, st);
     NW_TRY(sg.reserve(message_stage_bytes(total, n) + Stager::room(n * 64) + Stager::room(n * 32)), "pinned io");
-    int rc = upload_messages(ctx, ws, sg, msg, len, n, total);
+    int rc = upload_messages(ctx, ws, sg, msg, len, n, total, fixed_len);
     if (rc != NW_OK) return rc;
     NW_TRY(ws->ensure(ws->w_sig, n * 64 + 64), "ws sig");
     NW_TRY(ws->ensure(ws->w_keys, n * 32 + 32), "ws keys");
@@ -1087,14 +1107,15 @@ int run_generic(nw_ctx* ctx, const uint8_t* const* msg, const size_t* len, const
     const bool cached = lookup_slots(ctx, pk, n, slots.data());
     int rc = NW_OK;
     if (!cached) {
-        rc = upload_sig_keys(ctx, ws, msg, len, pk, sig, n, st);
+        uint64_t flen = UINT64_MAX;
+        rc = upload_sig_keys(ctx, ws, msg, len, pk, sig, n, st, batch_mode ? &flen : nullptr);
         if (rc != NW_OK) return rc;
         NW_TRY(ws->ensure(ws->w_ok, n + 16), "ws ok");
         if (batch_mode) {
             NW_TRY(ws->ensure(ws->w_cert_ok, 16), "ws verdict");
             const uint32_t cnt = (uint32_t)n;
             rc = enqueue_msm(ctx, ws, 1, &cnt, n, zseed, batch_index, 0, ws->w_cert_ok.as<uint8_t>(), nullptr, nullptr,
-                             st);
+                             st, flen);
             if (rc != NW_OK) return rc;
         } else {
             rc = enqueue_strict_var(ctx, ws, n, st, ws->w_ok.as<uint8_t>());
@@ -1427,11 +1448,12 @@ int nw_verify_batches_pk(nw_ctx* ctx, size_t nb, const uint32_t* counts, const u
     if (!ws) return NW_ERR_DEVICE;
     hipStream_t st = ws->stream;
     NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
-    int rc = upload_sig_keys(ctx, ws, msg, len, pk, sig, nsig, st);
+    uint64_t flen = UINT64_MAX;
+    int rc = upload_sig_keys(ctx, ws, msg, len, pk, sig, nsig, st, &flen);
     if (rc != NW_OK) return rc;
     NW_TRY(ws->ensure(ws->w_cert_ok, nb + 16), "ws verdicts");
     rc = enqueue_msm(ctx, ws, nb, counts, nsig, zseed, batch_base, 0, ws->w_cert_ok.as<uint8_t>(), nullptr, nullptr,
-                     st);
+                     st, flen);
     if (rc != NW_OK) return rc;
     NW_TRY(hipMemcpyAsync(batch_ok, ws->w_cert_ok.p, nb, hipMemcpyDeviceToHost, st), "D2H verdicts");
     NW_TRY(hipStreamSynchronize(st), "sync");
@@ -1452,12 +1474,14 @@ int nw_verify_batch_partial(nw_ctx* ctx, const uint8_t* const* msg, const size_t
     if (!ws) return NW_ERR_DEVICE;
     hipStream_t st = ws->stream;
     NW_TRY(lease.bind(st, true), "hipStreamWaitEvent");
-    int rc = upload_sig_keys(ctx, ws, msg, len, pk, sig, n, st);
+    uint64_t flen = UINT64_MAX;
+    int rc = upload_sig_keys(ctx, ws, msg, len, pk, sig, n, st, &flen);
     if (rc != NW_OK) return rc;
     NW_TRY(ws->ensure(ws->w_out, MSM_PT_WORDS * 4 + 16), "ws point");
     const uint32_t cnt = (uint32_t)n;
     uint32_t* d_bad = nullptr;
-    rc = enqueue_msm(ctx, ws, 1, &cnt, n, zseed, batch_index, z_offset, nullptr, ws->w_out.as<uint32_t>(), &d_bad, st);
+    rc = enqueue_msm(ctx, ws, 1, &cnt, n, zseed, batch_index, z_offset, nullptr, ws->w_out.as<uint32_t>(), &d_bad, st,
+                     flen);
     if (rc != NW_OK) return rc;
     uint32_t hbad = 0;
     NW_TRY(hipMemcpyAsync(point, ws->w_out.p, NW_POINT_BYTES, hipMemcpyDeviceToHost, st), "D2H point");

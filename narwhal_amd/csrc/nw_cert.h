@@ -1,6 +1,7 @@
 // Certificate verdicts of the batch equation, by one wave per certificate: the finalize (flag
 // reduction, stake sum, verdict whenever the flags decide it) and the exact sum over slow-path
-// terms.  Shared by k_cert_finalize / k_cert_exact / k_cert_tail (nw_kernels.hip) and by the
+// terms.  LDS exchanges between the wave's lanes use wave_lds_sync (nw_core.h): a caller may run a
+// certificate on one wave of a workgroup whose other waves have finished.  Shared by k_cert_finalize / k_cert_exact / k_cert_tail (nw_kernels.hip) and by the
 // small-call exact-path kernel k_slow_tail (nw_verify_kernels.h).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -9,14 +10,6 @@
 #include "nw_core.h"
 
 namespace nw {
-
-// LDS exchange between the lanes of ONE wave (every caller below runs a certificate on a single
-// wave, possibly inside a larger workgroup whose other waves have finished): the LDS stores are
-// complete before the loads issue, no workgroup barrier.
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-}
 
 // Per-certificate verdict: definitive Err on any bad S / undecodable A / undecodable R, else the
 // exact remaining batch sum (usually empty) must be the identity.  One 64-lane wave per

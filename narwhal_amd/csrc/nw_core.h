@@ -8,6 +8,15 @@
 
 namespace nw {
 
+// Ordering between the lanes of ONE wave (LDS or global data other lanes of the wave wrote):
+// workgroup-scope fences (they wait for the wave's outstanding memory operations) around a
+// wave-level barrier; replaces __syncthreads where the block's other waves are independent or gone.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // Batch coefficient z_i of vote i of certificate ``cert`` (NW-Z v1: nonce = global certificate index).
 __device__ __forceinline__ void coeff_z(const VerifyParams& a, uint32_t i, uint32_t cert, uint32_t z4[4]) {
     const uint64_t bidx = a.cert_base + cert;

@@ -38,6 +38,8 @@ struct MsmParams {
     const uint8_t* msg_base;       // packed messages
     const uint64_t* msg_off;       // [nsig]
     const uint64_t* msg_len;       // [nsig]
+    uint64_t msg_flen;             // UINT64_MAX: msg_off / msg_len; else every message has this length,
+                                   // back to back from msg_base (the arrays are not uploaded)
     uint64_t batch_base;           // NW-Z v1 nonce of batch 0
     uint32_t z_off;                // NW-Z v1 counter offset (a shard of one huge batch)
     uint32_t zseed[8];
@@ -52,6 +54,8 @@ struct MsmParams {
     uint32_t* part;                // [ntasks][2][64][40] run partials at lane-slice boundaries
     uint32_t* wpart;               // [ntasks][40] window partial sums
     const uint32_t* wfirst;        // [nb * nwin_a + 1] first window partial of (b, win)
+    uint32_t one_task_windows;     // every (b, win) has exactly one task, task index b * nwin_a + win:
+                                   // its partial IS the window sum (k_msm_wsum skipped)
     // final
     const uint32_t* btab;          // basepoint comb
     uint8_t* batch_ok;             // [nb] verdicts (may be null)

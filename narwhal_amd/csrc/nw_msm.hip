@@ -3,8 +3,8 @@
 // Batch path (dalek::verify_batch, the cofactorless equation with seeded z_i):
 //     sum_i z_i R_i + sum_i (z_i h_i mod l) A_i - (sum_i z_i s_i mod l) B == O
 // evaluated literally as a segmented Pippenger MSM over the 2n points {R_i, A_i} of every batch:
-//   k_msm_prep     one lane per signature: S parse, R and A decompression, h_i, z_i, a_i = z_i h_i
-//                  mod l, signed radix-2^C digits of z_i and a_i, affine Niels entries;
+//   k_msm_prep     two lanes per signature (R / A decompressed side by side): S parse, h_i, z_i,
+//                  a_i = z_i h_i mod l, signed radix-2^C digits of z_i and a_i, affine Niels entries;
 //   k_msm_bucket   one wave per (batch, window, chunk of <= MSM_CH entries), four per workgroup: LDS counting sort of
 //                  the chunk by |digit|, each lane accumulates an equal slice of the sorted list
 //                  (runs that cross slice boundaries are merged afterwards), then the bucket
@@ -256,10 +256,19 @@ __global__ void __launch_bounds__(QUAD ? 64 : 256) k_verify_var(VerifyParams a, 
 }
 
 // ------------------------------------------------------------------------------------ MSM
+// Two lanes per signature (side = lane & 1): both run the hash, the scalars and the recoding
+// (uniform code, a few thousand instructions), and each decompresses ONE point (side 0: R, side 1:
+// A).  The two pow chains (~19 k instructions each) were the lane's time: one lane per signature
+// gave 977 waves for 1,024 SIMDs at the MSM leg's 62,500 signatures, each running both chains
+// back to back at the lone-wave rate.
+#ifndef NW_MSM_PREP_WAVES
+#define NW_MSM_PREP_WAVES 2   // waves per SIMD the register allocation must allow (A/B: 1)
+#endif
 template <int C>
-__global__ void __launch_bounds__(256) k_msm_prep(MsmParams a) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.nsig) return;
+__global__ void __launch_bounds__(256, NW_MSM_PREP_WAVES) k_msm_prep(MsmParams a) {
+    const uint32_t gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t i = gt >> 1, side = gt & 1u;
+    if (i >= a.nsig) return;   // both lanes of a pair leave together
     const uint32_t b = a.sig_batch[i];
     const uint32_t f = a.bfirst[b], n = a.bcount[b], t = i - f;
     uint32_t R[8], S[8], Aw[8], h[8];
@@ -268,43 +277,44 @@ __global__ void __launch_bounds__(256) k_msm_prep(MsmParams a) {
     load_w8(Aw, a.keys + (size_t)i * 8);
     {
         uint32_t hw[16];
-        hram_generic(hw, R, Aw, a.msg_base + a.msg_off[i], a.msg_len[i]);
+        const bool fixed = a.msg_flen != ~0ull;
+        const uint64_t mo = fixed ? (uint64_t)i * a.msg_flen : a.msg_off[i];
+        hram_generic(hw, R, Aw, a.msg_base + mo, fixed ? a.msg_flen : a.msg_len[i]);
         sc_reduce512(h, hw);
     }
     const bool sok = sc_is_canonical(S);
-    ge_p3 Rp, Ap;
-    const bool rok = ge_decompress(Rp, R);
-    const bool aok = ge_decompress(Ap, Aw);
-    const bool ok = sok && rok && aok;
-    if (!ok) atomicOr(&a.bad[b], 1u);
+    uint32_t Yw[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) Yw[k] = side ? Aw[k] : R[k];
+    ge_p3 Pt;
+    const bool pok = ge_decompress(Pt, Yw);
+    const bool qok = __shfl_xor(pok ? 1 : 0, 1, 64) != 0;   // the pair's other point
+    const bool ok = sok && pok && qok;
+    if (!ok && side == 0) atomicOr(&a.bad[b], 1u);
     uint32_t z4[4];
     const uint64_t bidx = a.batch_base + b;
     chacha20_z(z4, a.zseed, t + a.z_off, (uint32_t)bidx, (uint32_t)(bidx >> 32), 0u);
     uint32_t z8[8] = {z4[0], z4[1], z4[2], z4[3], 0u, 0u, 0u, 0u};
-    uint32_t ai[8];
-    sc_mul(ai, z8, h);
-    uint32_t zs[12];
-    mulw<4, 8>(zs, z4, S);
+    uint32_t ks[8];
+    if (side) {
+        sc_mul(ks, z8, h);   // a_i = z_i h_i mod l
+    } else {
 #pragma unroll
-    for (int k = 0; k < 12; ++k) a.zs[(size_t)k * a.nsig + i] = ok ? zs[k] : 0u;
-    const size_t eR = 2 * (size_t)f + t, eA = 2 * (size_t)f + n + t;
-    if (ok) {
-        store_niels_affine(a.ent + eR * MSM_ENT_WORDS, Rp);
-        store_niels_affine(a.ent + eA * MSM_ENT_WORDS, Ap);
+        for (int k = 0; k < 8; ++k) ks[k] = z8[k];
+        uint32_t zs[12];
+        mulw<4, 8>(zs, z4, S);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) a.zs[(size_t)k * a.nsig + i] = ok ? zs[k] : 0u;
     }
+    const size_t e = 2 * (size_t)f + (side ? n : 0u) + t;   // R entries, then the batch's A entries
+    if (ok) store_niels_affine(a.ent + e * MSM_ENT_WORDS, Pt);
     const size_t E = 2 * (size_t)a.nsig;
     constexpr int NA = msm_nwin_a(C), NR = msm_nwin_r(C);
     int carry = 0;
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-        const int d = next_digit<C>(z8, carry);
-        a.dig[(size_t)j * E + eR] = (int16_t)(ok ? d : 0);
-    }
-    carry = 0;
-#pragma unroll
     for (int j = 0; j < NA; ++j) {
-        const int d = next_digit<C>(ai, carry);
-        a.dig[(size_t)j * E + eA] = (int16_t)(ok ? d : 0);
+        const int d = next_digit<C>(ks, carry);
+        if (side || j < NR) a.dig[(size_t)j * E + e] = (int16_t)(ok ? d : 0);
     }
 }
 
@@ -315,16 +325,6 @@ __global__ void __launch_bounds__(256) k_msm_prep(MsmParams a) {
 #ifndef MSM_BUCKET_WAVES
 #define MSM_BUCKET_WAVES 4
 #endif
-
-// Ordering between the lanes of ONE wave at a task's phase boundaries (LDS histogram / cursors /
-// sorted indices, and the global bucket and partial sums that other lanes of the wave wrote):
-// workgroup-scope fences (they wait for the wave's outstanding memory operations) around a
-// wave-level barrier replace __syncthreads, which would couple the block's independent waves.
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
 
 template <int C>
 __global__ void __launch_bounds__(64 * MSM_BUCKET_WAVES) k_msm_bucket(MsmParams a) {
@@ -511,8 +511,11 @@ __global__ void __launch_bounds__(64) k_msm_wsum(MsmParams a, uint32_t* wsum) {
     const uint32_t w0 = a.wfirst[bw], w1 = a.wfirst[bw + 1];
     ge_p3 acc = ge_identity();
     for (uint32_t w = w0 + L; w < w1; w += 64) acc = ge_add_p3(acc, load_p3(a.wpart + (size_t)w * MSM_PT_WORDS));
+    // only the levels that the partial count needs (lanes >= w1 - w0 hold the identity)
+    const uint32_t m = w1 - w0;
 #pragma unroll
-    for (unsigned off = 32; off > 0; off >>= 1) acc = ge_add_p3(acc, ge_shfl_down(acc, off));
+    for (unsigned off = 32; off > 0; off >>= 1)
+        if (off < m) acc = ge_add_p3(acc, ge_shfl_down(acc, off));
     if (L == 0) store_p3(wsum + (size_t)bw * MSM_PT_WORDS, acc);
 }
 
@@ -580,7 +583,7 @@ hipError_t launch_msm_c(const MsmParams& p, hipStream_t st) {
     // the metadata upload and no zs column is read, so wsum/final give the identity -> Ok, as
     // dalek's empty batch
     if (p.nsig) {
-        hipLaunchKernelGGL(k_msm_prep<C>, dim3(blocks_for(p.nsig, 256)), dim3(256), 0, st, p);
+        hipLaunchKernelGGL(k_msm_prep<C>, dim3(blocks_for(2 * (uint64_t)p.nsig, 256)), dim3(256), 0, st, p);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -591,11 +594,16 @@ hipError_t launch_msm_c(const MsmParams& p, hipStream_t st) {
         if (e != hipSuccess) return e;
     }
     constexpr int NA = msm_nwin_a(C);
-    // window sums live after the task partials in wpart
-    uint32_t* wsum = p.wpart + (size_t)p.ntasks * MSM_PT_WORDS;
-    hipLaunchKernelGGL(k_msm_wsum<C>, dim3(p.nb * NA), dim3(64), 0, st, p, wsum);
-    e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    // window sums live after the task partials in wpart; batches of up to MSM_CH / 2 signatures have
+    // one task per window, whose partial is already the window sum (the launch was ~48 us of shuffle
+    // levels adding identities)
+    uint32_t* wsum = p.wpart;
+    if (!p.one_task_windows) {
+        wsum = p.wpart + (size_t)p.ntasks * MSM_PT_WORDS;
+        hipLaunchKernelGGL(k_msm_wsum<C>, dim3(p.nb * NA), dim3(64), 0, st, p, wsum);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(k_msm_final<C>, dim3(p.nb), dim3(64), 0, st, p, (const uint32_t*)wsum);
     return hipGetLastError();
 }

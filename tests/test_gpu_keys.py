@@ -151,6 +151,39 @@ def test_uncached_worker_chunks_vs_oracle(bare):
     assert bare.committee_size() == 0
 
 
+@pytest.mark.parametrize("ml", [8, 32])
+def test_uncached_fixed_length_messages_vs_oracle(bare, ml):
+    """Messages of one length back to back in one buffer (numpy rows, as bench.py's msm leg and a
+    Rust caller with a flat buffer): the upload sends the block alone and k_msm_prep addresses
+    message i at i * len.  Verdicts equal the per-message upload's (separate bytes objects) and the
+    oracle's, with bad signatures in some chunks."""
+    import numpy as np
+    rng = random.Random(41 + ml)
+    count = 700
+    seeds = [bytes(rng.randrange(256) for _ in range(32)) for _ in range(count)]
+    msgs = [bytes(rng.randrange(256) for _ in range(ml)) for _ in range(count)]
+    pks, sigs = bare.sign_many(seeds, msgs)
+    bad = (3, 250, 251, 699)
+    for i in bad:
+        s = bytearray(sigs[i])
+        s[41] ^= 2
+        sigs[i] = bytes(s)
+    chunks = [(count * (c + 1)) // 16 - (count * c) // 16 for c in range(16)]
+    zseed = bytes(rng.randrange(256) for _ in range(32))
+    listed = bare.verify_batches_pk(chunks, msgs, pks, sigs, zseed, 77)
+    flat = np.frombuffer(b"".join(msgs), np.uint8).reshape(count, ml)
+    call = bare.prepare_batches_pk_call(chunks, flat, np.frombuffer(b"".join(pks), np.uint8).reshape(count, 32),
+                                        np.frombuffer(b"".join(sigs), np.uint8).reshape(count, 64))
+    fixed = [bool(x) for x in call(zseed, 77)]
+    firsts = [sum(chunks[:c]) for c in range(16)]
+    want = [all(not (f <= i < f + n) for i in bad) for f, n in zip(firsts, chunks)]
+    assert listed == want and fixed == want
+    for c in (0, 5, 15):
+        f, n = firsts[c], chunks[c]
+        zs = o.batch_coefficients(zseed, 77 + c, n)
+        assert o.verify_batch_z(msgs[f:f + n], sigs[f:f + n], pks[f:f + n], zs) == want[c]
+
+
 @pytest.mark.parametrize("ragged", [False, True])
 def test_uncached_large_call_vs_small_calls(bare, ragged):
     """One 20,000-signature nw_verify_batches_pk call (multi-chunk windows in every batch): the
