@@ -880,12 +880,22 @@ hipError_t staged_h2d(uint8_t* h, uint8_t* dst, const uint8_t* src, size_t n, hi
                         h, dst, st);
 }
 
+// Mid-size uploads (an uncached-key call's 4 MB of signatures) go in kPutPiece pieces, each DMA
+// issued once its piece is staged, so the memcpy of one piece runs under the DMA of the previous.
+constexpr size_t kPutPiece = 1u << 20;
+
 hipError_t Stager::put(void* dst, const void* src, size_t n) {
     if (!n) return hipSuccess;
     uint8_t* h = alloc(n);
     if (n >= kStageParallelMin) return staged_h2d(h, static_cast<uint8_t*>(dst), static_cast<const uint8_t*>(src), n, st_);
-    std::memcpy(h, src, n);
-    return copy(dst, h, n);
+    const size_t piece = n >= 2 * kPutPiece ? kPutPiece : n;
+    for (size_t o = 0; o < n; o += piece) {
+        const size_t m = std::min(piece, n - o);
+        std::memcpy(h + o, static_cast<const uint8_t*>(src) + o, m);
+        const hipError_t e = copy(static_cast<uint8_t*>(dst) + o, h + o, m);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
 
 size_t message_bytes(const size_t* len, size_t n) {
