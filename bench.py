@@ -160,14 +160,14 @@ def cpu_thread_candidates():
     return sorted({min(aff, base), min(aff, 2 * base)})
 
 
-def cpu_baseline(cs, com, seconds, probe_seconds=2.5, label="C2"):
+def cpu_baseline(cs, com, seconds, probe_seconds=2.5, label="C2", threads=None):
     """Oracle restatement timed on the host cores (rank 0, at every world size, after the timed
     region): bounded sample of certificates.  A short sweep over the candidate thread counts (cpu_thread_candidates; forced
     with NW_CPU_THREADS) picks the host's best rate, which is then timed on the main sample."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import nw_ref   # C restatement of dalek's u64 backend (oracle/nw_ref.c); test/baseline only
     zseed = bytes(32)
-    forced = int(os.environ.get("NW_CPU_THREADS", "0"))
+    forced = threads or int(os.environ.get("NW_CPU_THREADS", "0"))
     cands = [forced] if forced else cpu_thread_candidates()
 
     def run(threads, secs):
@@ -267,11 +267,12 @@ def host_fed(eng, cs, slots, zseed, chunks=16, threads=8, reps=5, stream_passes=
     call leases its own workspace and stream, so one call's upload overlaps another's kernels).
 
     value: STREAMING, the calls of ``stream_passes`` passes submitted back to back on the same threads
-    (a node's Core keeps submitting as batches arrive; no barrier between passes).  passes: the same
-    calls with a barrier after every pass (ms_reps), on reused and on freshly allocated buffers.  Copy
-    stalls (every calling thread inside hipMemcpyAsync for 5-13 ms while the GPU idles: HIP API trace,
-    profiles/r05/host_fed_r05.txt) concentrate in the first streaming round after start-up, so one
-    untimed streaming round runs first."""
+    (a node's Core keeps submitting as batches arrive; no barrier between passes), every pass on its
+    OWN host arrays, allocated after the warm-up round and touched by no earlier call.  first_round:
+    the same streaming round as the very first host-buffer work of the process (the warm-up, on
+    separate arrays): copy stalls (calling threads inside hipMemcpyAsync for 5-13 ms while the GPU
+    idles: HIP API trace, profiles/r05/host_fed_r05.txt) concentrate there.  passes: the same calls
+    with a barrier after every pass (ms_reps), on reused and on freshly allocated buffers."""
     from concurrent.futures import ThreadPoolExecutor
     import numpy as np
     bounds = np.linspace(0, cs.ncerts, chunks + 1).astype(int)
@@ -288,20 +289,20 @@ def host_fed(eng, cs, slots, zseed, chunks=16, threads=8, reps=5, stream_passes=
     def fresh(ps):   # new host buffers, as a node's network receives would hand over
         return [(a, b, c.copy(), d.copy(), e.copy(), f) for a, b, c, d, e, f in ps]
 
-    fresh_sets = [fresh(parts) for _ in range(reps)]
-    stream_sets = [fresh(parts) for _ in range(4)]
+    warm_sets = [fresh(parts) for _ in range(4)]
     with ThreadPoolExecutor(threads) as ex:
-        # warm-up, untimed: one streaming round over every set.  The first streaming round after
-        # start-up stalls (16-48 of its 320 calls take 5-11 ms, every thread inside hipMemcpyAsync
-        # with the GPU idle: 212-304 M sigs/s); every later round runs clean at 434-500 M with no call
-        # over 5 ms (tools/host_fed_stream_probe.py, profiles/r05/host_fed_r05.txt).  The workspace
-        # pool is already full-sized after the single-pass warm-up, so the stall is start-up state
-        # of the runtime's copy path; a running node is past it.
-        assert all(ex.map(run, [p for k in range(stream_passes) for p in stream_sets[k % len(stream_sets)]]))
+        # the first streaming round of the process (warm-up, timed for the record, its own arrays)
         t0 = time.perf_counter()
-        ok = all(ex.map(run, [p for k in range(stream_passes) for p in stream_sets[k % len(stream_sets)]]))
+        assert all(ex.map(run, [p for k in range(stream_passes) for p in warm_sets[k % len(warm_sets)]]))
+        t_first = time.perf_counter() - t0
+        del warm_sets
+        stream_sets = [fresh(parts) for _ in range(stream_passes)]    # untouched by any call so far
+        fresh_sets = [fresh(parts) for _ in range(reps)]
+        t0 = time.perf_counter()
+        ok = all(ex.map(run, [p for k in range(stream_passes) for p in stream_sets[k]]))
         t_stream = time.perf_counter() - t0
         assert ok
+        del stream_sets
         ts, tf = [], []
         for r in range(reps):
             t0 = time.perf_counter()
@@ -317,13 +318,17 @@ def host_fed(eng, cs, slots, zseed, chunks=16, threads=8, reps=5, stream_passes=
     dt = ts[len(ts) // 2]
     return {"value": stream_passes * cs.nsigs / t_stream, "unit": "sigs/s",
             "ms_per_pass_streaming": t_stream / stream_passes * 1e3,
+            "first_round": {"value": stream_passes * cs.nsigs / t_first, "ms_per_pass": t_first / stream_passes * 1e3,
+                            "note": "the same streaming round as the process's first host-buffer work (the warm-up, "
+                                    "4 rotating array sets of its own)"},
             "passes": {"value": cs.nsigs / dt, "ms": dt * 1e3, "ms_reps": [t * 1e3 for t in ts],
                        "fresh_buffers": {"value": cs.nsigs / tf[len(tf) // 2], "ms": tf[len(tf) // 2] * 1e3,
                                          "ms_reps": [t * 1e3 for t in tf]}},
             "note": "nw_verify_certs on pageable host buffers (every input staged through the call's pinned buffer), "
-                    "%d calls of ~%d signatures on %d threads; value: %d passes' calls streamed back to back on "
-                    "fresh host arrays (4 rotating sets) after one untimed streaming round; passes: a barrier after every pass, median of %d (reused "
-                    "arrays; fresh_buffers: newly allocated ones); PCIe and host packing included"
+                    "%d calls of ~%d signatures on %d threads; value: %d passes' calls streamed back to back, each "
+                    "pass on its own host arrays allocated after the warm-up round and never passed to the library "
+                    "before; passes: a barrier after every pass, median of %d (reused arrays; fresh_buffers: newly "
+                    "allocated ones); PCIe and host packing included"
                     % (chunks, cs.nsigs // chunks, threads, stream_passes, reps)}
 
 
@@ -673,13 +678,22 @@ def parse_args(argv):
                          "digests start when step i's verify kernels end), so a batch's serial SHA-512 chain "
                          "bounds its latency but not the step")
     ap.add_argument("--timing-only", action="store_true", help=argparse.SUPPRESS)   # A/B of timing-only variants
-    ap.add_argument("--hw-queues", type=int, default=0, help="set GPU_MAX_HW_QUEUES (<= 32) before HIP starts")
+    ap.add_argument("--hw-queues", type=int, default=0, help="set GPU_MAX_HW_QUEUES (1..32) before HIP starts")
+    ap.add_argument("--c4-steps", type=int, default=8,
+                    help="C2 runs: timed steps of the C4 leg (the north-star config, configs[3]) run after the C2 "
+                         "engine is closed; 0 disables it")
+    ap.add_argument("--c4-warmup", type=int, default=2)
+    ap.add_argument("--cpu-latency-samples", type=int, default=100,
+                    help="calls per one-thread CPU latency comparator (cpu_baseline.latency)")
     ap.add_argument("--engine-flags", type=lambda x: int(x, 0), default=0, help=argparse.SUPPRESS)   # nw_opts.flags (A/B)
     ap.add_argument("--key-window", type=int, default=-1,
                     help="key comb window; -1 = committee mode (library sizes it for the loaded committee)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher check without a GPU: ranks meet over gloo, rank 0 prints the world")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.hw_queues and not 1 <= a.hw_queues <= 32:
+        ap.error("--hw-queues must be in 1..32 (the GPU box refuses GPU_MAX_HW_QUEUES above 32)")
+    return a
 
 
 def config_plan(args, world, rank):
@@ -742,14 +756,15 @@ def timeit_once(fn):
     return time.perf_counter() - t0
 
 
-def latency_legs(eng, com, slots, cs, samples):
+def latency_legs(eng, com, slots, cs, samples, keep=None):
     """One-call latencies of the paths the Rust shim calls, host buffers, the
     call marshalled once so only the ABI call is timed:
       * strict: crypto::Signature::verify (crypto/src/lib.rs:200-204) -> nw_verify_strict, one
         header/vote signature (primary/src/core.rs:313,335), key in the committee cache and not;
       * batch: crypto::Signature::verify_batch (crypto/src/lib.rs:206-219) -> nw_verify_batch, one
         2f+1 certificate at 67 / 667 / 6,667 votes (committee cached), and 67 votes with keys
-        outside the cache (Pippenger MSM)."""
+        outside the cache (Pippenger MSM).
+    ``keep`` (a dict) receives the inputs of the calls the CPU comparator repeats (cpu_latency)."""
     import numpy as np
     from narwhal_amd import _lib, workload
 
@@ -769,6 +784,14 @@ def latency_legs(eng, com, slots, cs, samples):
     msg, pk, sig = bytes(cs.msgs[0]), bytes(com.pks[cs.signer[0]]), bytes(cs.sigs[0])
     assert eng.verify_strict(msg, pk, sig)
     out["strict_cached"] = p50(lambda: eng.verify_strict(msg, pk, sig), samples)
+    keep = {} if keep is None else keep
+    keep["strict"] = (msg, pk, sig)
+    keep["certs"] = {}
+
+    def keep_cert(c_com, c_cs, c):
+        f, n = int(c_cs.cert_first[c]), int(c_cs.cert_n[c])
+        keep["certs"][n] = (bytes(c_cs.msgs[c]), [bytes(c_com.pks[k]) for k in c_cs.signer[f:f + n]],
+                            [bytes(x) for x in c_cs.sigs[f:f + n]])
     fseed = np.frombuffer(os.urandom(32), np.uint8).reshape(1, 32)
     fpk, fsig = eng.sign_many_np(fseed, np.frombuffer(msg, np.uint8).reshape(1, 32))
     fpk, fsig = bytes(fpk[0]), bytes(fsig[0])
@@ -785,6 +808,7 @@ def latency_legs(eng, com, slots, cs, samples):
     call = cert_call(eng, com, cs, 0)
     assert call(zseed, 0)
     out["batch_cached_%d" % int(cs.cert_n[0])] = p50(lambda: call(zseed, 0), samples)
+    keep_cert(com, cs, 0)
     # keys outside the cache: a fresh committee of the same size that is never loaded
     nu = int(cs.cert_n[0])
     useeds = np.frombuffer(os.urandom(32 * nu), np.uint8).reshape(nu, 32).copy()
@@ -799,6 +823,8 @@ def latency_legs(eng, com, slots, cs, samples):
     import hashlib
     pre = os.urandom(32 + 8 + 6667 * 32)
     assert eng.sha512(pre) == hashlib.sha512(pre).digest()
+    keep["header"] = pre
+    keep["worker_batch"] = workload.worker_batches_np(1)[0].tobytes()
     out["header_digest_6667_parents"] = dict(p50(lambda: eng.sha512(pre), max(20, samples // 4)),
                                              bytes=len(pre),
                                              hashlib_1core_ms=min(timeit_once(lambda: hashlib.sha512(pre).digest())
@@ -810,6 +836,7 @@ def latency_legs(eng, com, slots, cs, samples):
         votes = 2 * nval // 3 + 1
         k_cs = workload.make_certificates(c2, 2, votes, e2)
         kc = cert_call(e2, c2, k_cs, 0)
+        keep_cert(c2, k_cs, 0)
         assert kc(zseed, 0)
         out["batch_cached_%d" % votes] = dict(p50(lambda: kc(zseed, 0), max(20, samples // 4)),
                                               key_window=e2.key_window())
@@ -817,6 +844,420 @@ def latency_legs(eng, com, slots, cs, samples):
         e2.close()
     out["note"] = ("host buffers, one ABI call per sample (marshalled once); cached = keys in the committee key "
                    "cache (nw_committee_load at spawn), uncached = variable-base path (k_verify_var / MSM)")
+    return out
+
+
+NW_F_STRICT = 0x008   # include/nwcrypto.h: the verify_strict verdict bit of a signature's flags
+
+
+def leg_args(args, config, **kw):
+    """A copy of ``args`` for another config's leg: that config's own shape (no overrides)."""
+    d = dict(vars(args))
+    d.update(config=config, validators=None, certs=None, votes=None, streams=None)
+    d.update(kw)
+    return argparse.Namespace(**d)
+
+
+class ConfigRun:
+    """One BASELINE config's timed step on this rank: engine, committee and
+    certificates resident in HBM; the step = nw_verify_certs_dev (+ C4: the rank's worker-batch
+    digests on a second stream, worker/src/processor.rs:65) (+ N > 1: the RCCL all-gathers of the
+    verdict bitmaps, stake and digests); the warm-up, the timed loop, and the read-back of EVERY
+    step's verdicts, accepted stake and input-check status (each step writes its own result set),
+    the last step's per-vote flags on every stream and, C4, all digests of the last two steps."""
+
+    def __init__(self, args, world, rank, local):
+        import numpy as np
+        import torch
+        from narwhal_amd import _lib, workload
+        t0 = time.perf_counter()
+        self.args, self.world, self.rank = args, world, rank
+        self.plan = plan = config_plan(args, world, rank)
+        self.dev = dev = torch.device("cuda", local)
+        self.eng = eng = _lib.Engine(device=local, key_window=args.key_window, flags=args.engine_flags)
+        self.com = com = workload.make_committee(plan["validators"], eng)
+        self.slots = slots = eng.committee_load_np(com.pks, com.stake)
+        self.first_cert = plan["first_cert"]                # each rank: its own shard of certificates
+        self.cs = cs = workload.make_certificates(com, plan["ncerts"], plan["votes"], eng, first_cert=self.first_cert)
+        self.ranges = plan["ranges"]                        # node-wide certificate ranges
+        self.d_sig = torch.from_numpy(cs.sigs).to(dev)
+        self.d_signer = torch.from_numpy(slots[cs.signer].astype(np.int32)).to(dev)
+        self.d_first = torch.from_numpy(cs.cert_first.astype(np.int32)).to(dev)
+        self.d_n = torch.from_numpy(cs.cert_n.astype(np.int32)).to(dev)
+        self.d_msg = torch.from_numpy(cs.msgs).to(dev)
+        # per-vote flags: one buffer per batch in flight; verdicts / stake / status: one set per step
+        self.nst = nst = max(1, args.streams if args.streams is not None else CONFIGS[args.config]["streams"])
+        self.flags = [torch.zeros(cs.nsigs, dtype=torch.int32, device=dev) for _ in range(nst)]
+        self.streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(nst - 1)]
+        self.scratch = self._result_set()
+        self.res = []
+        self.zseed = os.urandom(32)
+        # C4: the rank's worker-batch digests run inside the timed step on a second stream,
+        # concurrently with the verify kernels; the step ends when both are done
+        self.ndig = ndig = plan["digest_batches"]
+        self.from_host = bool(ndig) and args.batches == "host"
+        self.pipelined = bool(ndig) and not args.digest_join
+        if ndig:
+            self.host_b = workload.worker_batches_np(ndig)
+            self.blen = blen = self.host_b.shape[1]
+            self.d_boff = torch.arange(ndig, dtype=torch.int64, device=dev) * blen
+            self.d_blen = torch.full((ndig,), blen, dtype=torch.int64, device=dev)
+            # joined: one digest stream per batch in flight.  Pipelined: two alternating digest streams
+            # at high priority (step i + 1's digests run beside the tail of step i's), each with its
+            # output and, with host batches, its upload buffer (step i's batches are DMA'd on step i's
+            # digest stream)
+            ndst = 2 if self.pipelined else nst
+            self.d_bouts = [torch.empty((ndig, 64), dtype=torch.uint8, device=dev) for _ in range(ndst)]
+            self.s_digs = [torch.cuda.Stream(device=dev, priority=-1 if self.pipelined else 0) for _ in range(ndst)]
+            self.ev_digs = [torch.cuda.Event() for _ in range(ndst)]
+            if self.from_host:
+                self.uploader = BatchUploader(self.host_b, dev, nbuf=2,
+                                              copy_streams=self.s_digs if self.pipelined else None)
+                self.d_bdata = None
+            else:
+                self.d_bdata = torch.from_numpy(self.host_b.reshape(-1)).to(dev)
+        # N > 1: every all_gather on one stream (collectives of one communicator stay serialized),
+        # after its batch's kernels
+        self.s_comm = torch.cuda.Stream(device=dev) if world > 1 and nst > 1 else None
+        self.n_step = 0
+        self.ev_pre = None
+        torch.cuda.synchronize()       # inputs resident before any stream reads them
+        self.setup_s = time.perf_counter() - t0
+
+    def _result_set(self):
+        import torch
+        n = self.cs.ncerts
+        return (torch.zeros(n, dtype=torch.uint8, device=self.dev), torch.zeros(n, dtype=torch.int64, device=self.dev),
+                torch.zeros(1, dtype=torch.int32, device=self.dev))
+
+    def verify_step(self, stream, flags=None, res=None):
+        cs = self.cs
+        ok, stake, status = self.scratch if res is None else res
+        flags = self.flags[0] if flags is None else flags
+        self.eng.verify_certs_dev(cs.ncerts, self.d_first.data_ptr(), self.d_n.data_ptr(), cs.nsigs,
+                                  self.d_sig.data_ptr(), self.d_signer.data_ptr(), self.d_msg.data_ptr(), self.zseed,
+                                  self.first_cert, ok.data_ptr(), flags.data_ptr(), stake.data_ptr(),
+                                  stream.cuda_stream, d_status=status.data_ptr())
+
+    def step(self):
+        from narwhal_amd import shard
+        import torch
+        i = self.n_step
+        self.n_step += 1
+        cur, flags = self.streams[i % self.nst], self.flags[i % self.nst]
+        res = self.res[i] if i < len(self.res) else self.scratch
+        ndig, s_dig = self.ndig, None
+        if ndig:
+            # launched before the step's verify kernels, so the digest workgroups get their (exclusive)
+            # CUs first; the step ends when both are done.  (Not joining the streams per step, so
+            # that step i + 1's digests start while step i verifies, measured slower: 414-437 vs
+            # 486-491 M sigs/s, r04r: a digest launched while k_verify holds every CU waits for CUs;
+            # two alternating digest streams without the join, 460 M, r04u: the second stream's digest
+            # still started only when the first finished, then waited for CUs.)
+            di = i % len(self.s_digs)
+            s_dig, ev_dig = self.s_digs[di], self.ev_digs[di]
+            # Joined: after the previous step's verify kernels (a digest enqueued while k_verify holds
+            # every CU waits for whole CUs to drain: its workgroups take a CU each).  Pipelined: only
+            # after its own stream's earlier work (step i-2's digests, this step's upload), so it is
+            # queued while step i-1's k_verify still runs and takes CUs as that grid's dispatch ends,
+            # ahead of step i's k_verify (which waits for step i-1's k_finish); when both became ready
+            # at the same event, the verify grid won the CUs in about one run in three and the digests
+            # ran 26.7 instead of 16-17 ms (profiles/r05/c4_hwq_r05.txt)
+            if not self.pipelined:
+                s_dig.wait_stream(cur)
+            elif self.ev_pre is not None:
+                s_dig.wait_event(self.ev_pre)   # no earlier than step i-1's verify kernels (HBM batches
+                #                                 would otherwise let the digest streams run steps ahead)
+            src = self.uploader.ready_buffer(s_dig) if self.from_host else self.d_bdata
+            self.eng.sha512_many_dev(src.data_ptr(), self.d_boff.data_ptr(), self.d_blen.data_ptr(), ndig,
+                                     self.d_bouts[di].data_ptr(), s_dig.cuda_stream)
+            ev_dig.record(s_dig)
+        if self.pipelined:
+            self.ev_pre = torch.cuda.Event()
+            self.ev_pre.record(cur)             # this step's verify kernels start here
+        self.verify_step(cur, flags, res)
+        if self.from_host:
+            # host threads stage the NEXT step's batches into pinned memory and DMA them while this
+            # step's kernels run (the next step's digests wait for that upload; the timed region's
+            # closing synchronize waits for every upload)
+            self.uploader.stage_next(read_stream=s_dig)
+        if ndig and not self.pipelined:
+            cur.wait_event(ev_dig)
+        if self.world > 1:
+            # RCCL all_gathers of the verdict bitmaps + stake and (C4) of the ranks' worker digests
+            # (32 B per batch), after this step's kernels.  Pipelined: the digests all-gathered in
+            # step i are step i - 1's (finished while step i verified); the last step's after the loop
+            dig_out = None
+            if ndig and not self.pipelined:
+                dig_out = self.d_bouts[i % len(self.d_bouts)]
+            elif ndig and i > 0:
+                dig_out = self.d_bouts[(i - 1) % len(self.d_bouts)]
+                cur.wait_event(self.ev_digs[(i - 1) % len(self.ev_digs)])
+            if self.s_comm is None:
+                if dig_out is not None:
+                    shard.allgather_digests(dig_out)
+                shard.allgather_verdicts(res[0], res[1], self.ranges)
+            else:
+                self.s_comm.wait_stream(cur)
+                with torch.cuda.stream(self.s_comm):
+                    if dig_out is not None:
+                        shard.allgather_digests(dig_out)
+                    shard.allgather_verdicts(res[0], res[1], self.ranges)
+                cur.wait_stream(self.s_comm)
+
+    def drain_digests(self):
+        """Pipelined C4: the last step's digests (and, N > 1, their all-gather) inside the timed region."""
+        from narwhal_amd import shard
+        if not self.pipelined or self.n_step == 0:
+            return
+        i = self.n_step - 1
+        cur = self.streams[i % self.nst]
+        cur.wait_event(self.ev_digs[i % len(self.ev_digs)])
+        if self.world > 1:
+            shard.allgather_digests(self.d_bouts[i % len(self.d_bouts)])
+
+    def run(self, steps, warmup):
+        """W untimed warm-up steps, then EXACTLY ``steps`` steps bracketed by a barrier and a
+        synchronize on both sides; returns (max-over-ranks seconds, output checks)."""
+        import torch
+        import torch.distributed as dist
+        self.res = [self._result_set() for _ in range(warmup + steps)]
+        if self.from_host:
+            self.uploader.stage_next(read_stream=None)   # the first step's batches
+        torch.cuda.synchronize()
+        for _ in range(warmup):
+            self.step()
+        if self.ndig:
+            self.drain_digests()
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        self.eng.profile_read()             # discard warm-up events
+        self.eng.profile_enable(True)
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            self.step()
+        if self.ndig:
+            self.drain_digests()
+        torch.cuda.synchronize()
+        if self.world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        self.eng.profile_enable(False)
+        self.prof = self.eng.profile_read()
+        checks = self.check_outputs(warmup, steps)
+        if self.world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=self.dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            okt = torch.tensor([1 if checks["ok"] else 0], dtype=torch.int32, device=self.dev)
+            dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+            checks["ok_all_ranks"] = bool(okt.item())
+        self.steps, self.warmup, self.elapsed = steps, warmup, elapsed
+        return elapsed, checks
+
+    def expected_digests(self):
+        """hashlib SHA-512 of this rank's worker batches (threads: hashlib releases the GIL)."""
+        import hashlib
+        import numpy as np
+        from concurrent.futures import ThreadPoolExecutor
+        with ThreadPoolExecutor(8) as ex:
+            ds = list(ex.map(lambda b: hashlib.sha512(b.data).digest(), self.host_b))
+        return np.frombuffer(b"".join(ds), np.uint8).reshape(len(ds), 64)
+
+    def check_outputs(self, warmup, steps):
+        """Every step's certificate verdicts, accepted stake and input-check status (the committee is
+        honest with stake 1 per key, so each certificate's accepted stake is its vote count), the
+        last step's per-vote flags on each stream (strict bit set), and C4's digests."""
+        import numpy as np
+        votes = self.plan["votes"]
+        bad = []
+        for k, (ok, stake, st) in enumerate(self.res):
+            if not (bool(ok.all().item()) and bool((stake == votes).all().item()) and int(st.item()) == 0):
+                bad.append(k)
+        used = min(self.nst, warmup + steps)
+        strict = all(bool(((f & NW_F_STRICT) != 0).all().item()) for f in self.flags[:used])
+        out = {"steps_checked": warmup + steps, "timed_steps_checked": steps, "bad_steps": bad,
+               "last_flags_all_strict": strict,
+               "what": "every step's %d certificate verdicts + accepted stake + status word (own result set per "
+                       "step), and the %d per-vote flags of the last step on each of %d stream(s)"
+                       % (self.cs.ncerts, self.cs.nsigs, used)}
+        dig_ok = True
+        if self.ndig:
+            exp = self.expected_digests()
+            nb = min(len(self.d_bouts), warmup + steps)
+            dig_ok = all(np.array_equal(d.cpu().numpy(), exp) for d in self.d_bouts[:nb])
+            out["digests_ok"] = dig_ok
+            out["digests_what"] = ("all %d digests written by the last %d step(s) vs hashlib SHA-512 of the batches"
+                                   % (self.ndig, nb))
+        out["ok"] = not bad and strict and dig_ok
+        return out
+
+    def isolated(self, launches=3):
+        """k_verify launched alone after the timed region, the GPU idle between launches."""
+        import torch
+        self.eng.profile_enable(True)
+        for _ in range(launches):
+            self.verify_step(self.streams[0])
+            torch.cuda.synchronize()
+        self.eng.profile_enable(False)
+        return self.eng.profile_read()
+
+    def roofline(self, iso, with_profiles):
+        """k_verify's fraction of the measured MAD peak (work model: kverify_fm_per_sig)."""
+        kms, kn, ksigs = self.prof
+        avg_launch_s = (kms / kn) / 1e3 if kn else float("nan")
+        if ksigs is None:                              # library without nw_profile_read_sigs (A/B runs)
+            ksigs = self.cs.nsigs * kn
+        sigs_per_launch = ksigs / kn if kn else 0.0
+        kw = self.eng.key_window()
+        bw = self.eng.base_window()
+        fm = kverify_fm_per_sig(kw, bw)
+        peak = valu_peak_mad_per_s() / 1e12
+        achieved = sigs_per_launch * fm * MADS_PER_FM / avg_launch_s / 1e12
+        v1 = COST_MODEL_V1_FM.get(self.plan["votes"])
+        nst = self.nst
+        return {
+            "bound": "valu", "kernel": "k_verify", "achieved": achieved, "peak": peak, "unit": "TMAD/s",
+            "frac": achieved / peak,
+            "traffic": traffic_per_launch() if with_profiles else None,
+            "per_cycle": clock_frac_profile() if with_profiles else None,
+            "avg_launch_ms": avg_launch_s * 1e3, "launches": kn,
+            "batches_in_flight": nst,
+            "isolated": None if not iso or not iso[1] else {
+                "avg_launch_ms": iso[0] / iso[1], "launches": iso[1],
+                "frac": sigs_per_launch * fm * MADS_PER_FM / (iso[0] / iso[1] / 1e3) / 1e12 / peak,
+                "note": "k_verify launched alone after the timed region, the GPU idle between launches (frac "
+                        "above: the timed launches, back to back%s)" % (
+                            ", overlapping the other batch's kernels" if nst > 1 else "")},
+            "work_model": "%.0f sigs/launch (%d launches per step) x %d FM/sig (7 FM per mixed addition x (%d basepoint "
+                          "+ %d key - 1) comb positions + 1 FM for the chain's first entry - 1 FM (no T in the last "
+                          "addition), key window %d) x 100 u32 MADs; SHA-512/mod-l/recoding VALU work not counted; "
+                          "peak = measured v_mad_u64_u32 rate"
+                          % (sigs_per_launch, kn // max(1, self.steps), fm, comb_pos(bw), comb_pos(kw), kw),
+            "dalek_equiv": {"fm_per_sig": v1, "TMADps": (sigs_per_launch * v1 * MADS_PER_FM / avg_launch_s / 1e12)
+                            if v1 else None,
+                            "note": "SURVEY §8(d) cost model v1 = dalek's MSM work per signature; the comb "
+                                    "algorithm needs %.1fx fewer FM" % (v1 / fm) if v1 else ""},
+        }
+
+    def workload_desc(self):
+        plan, cs = self.plan, self.cs
+        strong = plan["scaling"] == "strong"
+        desc = ("%s: %d-validator committee, %d certificates x %d votes (%d sigs) %s"
+                % (self.args.config, plan["validators"], plan["node_certs"] if strong else plan["ncerts"],
+                   plan["votes"], plan["total_sigs"] if strong else cs.nsigs,
+                   "per node round, partitioned over the GPUs" if strong else "per GPU"))
+        if self.ndig:
+            desc += " + %d worker-batch SHA-512 digests (%d B each) per GPU on a second stream" % (self.ndig, self.blen)
+            if self.from_host:
+                desc += (", batches from pageable host memory (staged to pinned + H2D inside the timed loop, "
+                         "double-buffered)")
+        return desc
+
+    def digest_in_step(self):
+        if not self.ndig:
+            return None
+        d = {"batches_per_gpu": self.ndig, "bytes_per_gpu_per_step": self.ndig * self.blen,
+             "GBps_per_gpu": self.ndig * self.blen * self.steps / self.elapsed / 1e9,
+             "batches_from_host": self.from_host}
+        if self.from_host:
+            d["upload"] = self.uploader.stats()
+        return d
+
+    def close(self):
+        """Release the engine (its key tables) and this run's device buffers."""
+        import torch
+        torch.cuda.synchronize()
+        self.eng.close()
+        for k in ("d_sig", "d_signer", "d_first", "d_n", "d_msg", "flags", "scratch", "res", "d_boff", "d_blen",
+                  "d_bouts", "d_bdata", "uploader"):
+            if hasattr(self, k):
+                setattr(self, k, None)
+        torch.cuda.empty_cache()
+
+
+def cert_latency(run, samples):
+    """Single-certificate latency through nw_verify_certs from host buffers (H2D -> kernels -> D2H),
+    the Core::run usage pattern; p50 / p99 over ``samples`` calls."""
+    import numpy as np
+    cs, lat = run.cs, []
+    for i in range(samples):
+        c = i % cs.ncerts
+        f, n = int(cs.cert_first[c]), int(cs.cert_n[c])
+        t1 = time.perf_counter()
+        cok, _, _ = run.eng.verify_certs_np(np.array([0], np.uint32), np.array([n], np.uint32), cs.sigs[f:f + n],
+                                            run.slots[cs.signer[f:f + n]], cs.msgs[c:c + 1], run.zseed,
+                                            run.first_cert + c)
+        lat.append(time.perf_counter() - t1)
+        assert cok[0] == 1
+    lat.sort()
+    return (lat[len(lat) // 2] * 1e3, lat[int(len(lat) * 0.99)] * 1e3) if lat else (None, None)
+
+
+def c4_block(run, elapsed, checks, iso):
+    """The north-star config's leg (configs[3]): one GPU's share of a 10,000-validator node round."""
+    plan = run.plan
+    total = plan["total_sigs"] * run.steps
+    kw = run.eng.key_window()
+    return {"config": run.workload_desc(), "baseline_config": plan["baseline"],
+            "value": total / elapsed, "unit": "sigs/s", "n_gpus": run.world, "steps": run.steps,
+            "warmup": run.warmup, "ms_per_step": elapsed / run.steps * 1e3, "scaling": plan["scaling"],
+            "key_window": kw, "key_negtab": run.eng.key_negtab(),
+            "kverify_fm_per_sig": kverify_fm_per_sig(kw, run.eng.base_window()),
+            "roofline": run.roofline(iso, False), "digest_in_step": run.digest_in_step(),
+            "checks": checks, "setup_s": run.setup_s}
+
+
+def cpu_latency(inp, gpu, samples=100):
+    """One-call latencies on ONE host thread, the reference's usage: Core verifies each header / vote
+    inline (primary/src/core.rs:306-346) with crypto::Signature::verify -> dalek verify_strict, each
+    certificate with Signature::verify_batch (crypto/src/lib.rs:200-219), and the worker hashes each
+    batch with SHA-512 (worker/src/processor.rs:65).  oracle/nw_ref.c is the C restatement of dalek
+    1.0.1 (strict: its double-base NAF5/NAF8 with the precomputed basepoint table; certificates:
+    per-vote key decompression + Straus below 190 points, Pippenger above); hashlib (OpenSSL) for the
+    digests.  Same inputs as the GPU calls; ``cpu_over_gpu`` > 1 means the GPU call is faster."""
+    import hashlib
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import nw_ref   # test/baseline only
+
+    def stats(fn, n):
+        for _ in range(3):
+            fn()
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        ts.sort()
+        return {"p50_ms": ts[len(ts) // 2] * 1e3, "p99_ms": ts[min(n - 1, int(n * 0.99))] * 1e3,
+                "min_ms": ts[0] * 1e3, "samples": n}
+
+    out = {}
+    msg, pk, sig = inp["strict"]
+    assert nw_ref.verify_strict(pk, msg, sig)
+    out["strict"] = stats(lambda: nw_ref.verify_strict(pk, msg, sig), 2 * samples)
+    zseed = bytes(32)
+    for votes, (digest, pks, sigs) in sorted(inp["certs"].items()):
+        call = nw_ref.prepare_crypto_verify_batch(digest, pks, sigs)
+        assert call(zseed, 0)
+        out["cert_%d" % votes] = stats(lambda: call(zseed, 0), samples)
+    batch = inp["worker_batch"]
+    out["worker_batch"] = dict(stats(lambda: hashlib.sha512(batch).digest(), samples), bytes=len(batch))
+    pre = inp["header"]
+    out["header_6667_parents"] = dict(stats(lambda: hashlib.sha512(pre).digest(), samples), bytes=len(pre))
+    for k, g in gpu.items():
+        if k in out and g:
+            out[k]["gpu_p50_ms"] = g[0]
+            out[k]["gpu_source"] = g[1]
+            out[k]["cpu_over_gpu"] = out[k]["p50_ms"] / g[0]
+    out["threads"] = 1
+    out["cpu_model"] = cpu_model()
+    out["note"] = ("one host thread, one call at a time (no batching across calls), p50/p99 over the samples; "
+                   "cpu_over_gpu = CPU p50 / GPU p50 of the same call on the same inputs (> 1: the GPU is faster)")
     return out
 
 
@@ -834,10 +1275,8 @@ def main(argv=None):
     if args.dry_run:
         return dry_run(args)
 
-    import numpy as np
     import torch
     import torch.distributed as dist
-    from narwhal_amd import shard
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -851,299 +1290,109 @@ def main(argv=None):
         gloo_group = dist.new_group(backend="gloo")   # host-side barrier for the CPU-baseline leg
 
     from narwhal_amd import _lib, workload
-    plan = config_plan(args, world, rank)
-    eng = _lib.Engine(device=local, key_window=args.key_window, flags=args.engine_flags)
-    com = workload.make_committee(plan["validators"], eng)
-    slots = eng.committee_load_np(com.pks, com.stake)
-    first_cert = plan["first_cert"]                     # each rank: its own shard of certificates
-    cs = workload.make_certificates(com, plan["ncerts"], plan["votes"], eng, first_cert=first_cert)
-    ranges = plan["ranges"]                             # node-wide certificate ranges
-
-    dev = torch.device("cuda", local)
-    d_sig = torch.from_numpy(cs.sigs).to(dev)
-    d_signer = torch.from_numpy(slots[cs.signer].astype(np.int32)).to(dev)
-    d_first = torch.from_numpy(cs.cert_first.astype(np.int32)).to(dev)
-    d_n = torch.from_numpy(cs.cert_n.astype(np.int32)).to(dev)
-    d_msg = torch.from_numpy(cs.msgs).to(dev)
-    # one output set per batch in flight (verdicts, flags, accepted stake, input-check status)
-    nst = max(1, args.streams if args.streams is not None else CONFIGS[args.config]["streams"])
-    outs = [dict(ok=torch.zeros(cs.ncerts, dtype=torch.uint8, device=dev),
-                 flags=torch.zeros(cs.nsigs, dtype=torch.int32, device=dev),
-                 stake=torch.zeros(cs.ncerts, dtype=torch.int64, device=dev),
-                 status=torch.zeros(1, dtype=torch.int32, device=dev)) for _ in range(nst)]
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream(device=dev) for _ in range(nst - 1)]
-    zseed = os.urandom(32)
-
-    def verify_step(stream, o=outs[0]):
-        eng.verify_certs_dev(cs.ncerts, d_first.data_ptr(), d_n.data_ptr(), cs.nsigs, d_sig.data_ptr(),
-                             d_signer.data_ptr(), d_msg.data_ptr(), zseed, first_cert, o["ok"].data_ptr(),
-                             o["flags"].data_ptr(), o["stake"].data_ptr(), stream.cuda_stream,
-                             d_status=o["status"].data_ptr())
-
-    # C4: the rank's worker-batch digests (worker/src/processor.rs:65) run inside the timed step on
-    # a second stream, concurrently with the verify kernels; the step ends when both are done
-    ndig = plan["digest_batches"]
-    from_host = bool(ndig) and args.batches == "host"
-    pipelined = bool(ndig) and not args.digest_join
-    if ndig:
-        import hashlib
-        host_b = workload.worker_batches_np(ndig)
-        blen = host_b.shape[1]
-        d_boff = torch.arange(ndig, dtype=torch.int64, device=dev) * blen
-        d_blen = torch.full((ndig,), blen, dtype=torch.int64, device=dev)
-        # joined: one digest stream per batch in flight.  Pipelined: two alternating digest streams
-        # at high priority (step i + 1's digests run beside the tail of step i's), each with its output
-        # and, with host batches, its upload buffer (step i's batches are DMA'd on step i's digest stream)
-        ndst = 2 if pipelined else nst
-        d_bouts = [torch.empty((ndig, 64), dtype=torch.uint8, device=dev) for _ in range(ndst)]
-        s_digs = [torch.cuda.Stream(device=dev, priority=-1 if pipelined else 0) for _ in range(ndst)]
-        ev_digs = [torch.cuda.Event() for _ in range(ndst)]
-        if from_host:
-            uploader = BatchUploader(host_b, dev, nbuf=2, copy_streams=s_digs if pipelined else None)
-            d_bdata = None
-        else:
-            d_bdata = torch.from_numpy(host_b.reshape(-1)).to(dev)
-
-    # N > 1: every all_gather on one stream (collectives of one communicator stay serialized), after
-    # its batch's kernels; a stream reuses its output set only after that set's all_gather
-    s_comm = torch.cuda.Stream(device=dev) if world > 1 and nst > 1 else None
-    n_step = [0]
-    ev_pre = [None]
-
-    def step():
-        i = n_step[0]
-        n_step[0] += 1
-        cur, o = streams[i % nst], outs[i % nst]
-        if ndig:
-            # launched before the step's verify kernels, so the digest workgroups get their (exclusive)
-            # CUs first; the step ends when both are done.  (Not joining the streams per step, so
-            # that step i + 1's digests start while step i verifies, measured slower: 414-437 vs
-            # 486-491 M sigs/s, r04r: a digest launched while k_verify holds every CU waits for CUs;
-            # two alternating digest streams without the join, 460 M, r04u: the second stream's digest
-            # still started only when the first finished, then waited for CUs.)
-            di = i % len(s_digs)
-            s_dig, ev_dig = s_digs[di], ev_digs[di]
-            # Joined: after the previous step's verify kernels (a digest enqueued while k_verify holds
-            # every CU waits for whole CUs to drain: its workgroups take a CU each).  Pipelined: only
-            # after its own stream's earlier work (step i-2's digests, this step's upload), so it is
-            # queued while step i-1's k_verify still runs and takes CUs as that grid's dispatch ends,
-            # ahead of step i's k_verify (which waits for step i-1's k_finish); when both became ready
-            # at the same event, the verify grid won the CUs in about one run in three and the digests
-            # ran 26.7 instead of 16-17 ms (profiles/r05/c4_hwq_r05.txt)
-            if not pipelined:
-                s_dig.wait_stream(cur)
-            elif ev_pre[0] is not None:
-                s_dig.wait_event(ev_pre[0])   # no earlier than step i-1's verify kernels (HBM batches
-                #                                would otherwise let the digest streams run steps ahead)
-            if from_host:
-                src = uploader.ready_buffer(s_dig)         # uploaded during the previous step
-            else:
-                src = d_bdata
-            eng.sha512_many_dev(src.data_ptr(), d_boff.data_ptr(), d_blen.data_ptr(), ndig,
-                                d_bouts[di].data_ptr(), s_dig.cuda_stream)
-            ev_dig.record(s_dig)
-        if pipelined:
-            ev_pre[0] = torch.cuda.Event()
-            ev_pre[0].record(cur)             # this step's verify kernels start here
-        verify_step(cur, o)
-        if from_host:
-            # host threads stage the NEXT step's batches into pinned memory and DMA them while this
-            # step's kernels run (the next step's digests wait for that upload; the timed region's
-            # closing synchronize waits for every upload)
-            uploader.stage_next(read_stream=s_dig)
-        if ndig and not pipelined:
-            cur.wait_event(ev_dig)
-        if world > 1:
-            # RCCL all_gathers of the verdict bitmaps + stake and (C4) of the ranks' worker digests
-            # (32 B per batch), after this step's kernels.  Pipelined: the digests all-gathered in
-            # step i are step i - 1's (finished while step i verified); the last step's after the loop
-            dig_out = None
-            if ndig and not pipelined:
-                dig_out = d_bouts[i % len(d_bouts)]
-            elif ndig and i > 0:
-                dig_out = d_bouts[(i - 1) % len(d_bouts)]
-                cur.wait_event(ev_digs[(i - 1) % len(ev_digs)])
-            if s_comm is None:
-                if dig_out is not None:
-                    shard.allgather_digests(dig_out)
-                shard.allgather_verdicts(o["ok"], o["stake"], ranges)
-            else:
-                s_comm.wait_stream(cur)
-                with torch.cuda.stream(s_comm):
-                    if dig_out is not None:
-                        shard.allgather_digests(dig_out)
-                    shard.allgather_verdicts(o["ok"], o["stake"], ranges)
-                cur.wait_stream(s_comm)
-
-    def drain_digests():
-        """Pipelined C4: the last step's digests (and, N > 1, their all-gather) inside the timed region."""
-        if not pipelined:
-            return
-        i = n_step[0] - 1
-        cur = streams[i % nst]
-        cur.wait_event(ev_digs[i % len(ev_digs)])
-        if world > 1:
-            shard.allgather_digests(d_bouts[i % len(d_bouts)])
-
-    if from_host:
-        uploader.stage_next(read_stream=None)   # the first step's batches
-    torch.cuda.synchronize()       # inputs resident before any stream reads them
-    for _ in range(args.warmup):
-        step()
-    if ndig:
-        drain_digests()
-    torch.cuda.synchronize()
-    ok_all = all(bool(o["ok"].all().item()) and bool((o["stake"] == plan["votes"]).all().item())
-                 and int(o["status"].item()) == 0 for o in outs[:min(nst, max(1, args.warmup))])
-    if ndig:
-        for b in (0, ndig - 1):
-            for d_bout in d_bouts[:min(len(d_bouts), max(1, args.warmup))]:
-                ok_all = ok_all and bytes(d_bout[b].cpu().numpy()) == hashlib.sha512(host_b[b].tobytes()).digest()
-    if world > 1:
-        dist.barrier()
-    eng.profile_read()             # discard warmup events
-    eng.profile_enable(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    if ndig:
-        drain_digests()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    eng.profile_enable(False)
-    kms, kn, ksigs = eng.profile_read()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        okt = torch.tensor([1 if ok_all else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok_all = bool(okt.item())
+    run = ConfigRun(args, world, rank, local)
+    plan = run.plan
+    elapsed, checks = run.run(args.steps, args.warmup)
     if not args.timing_only:
-        assert ok_all, "honest workload rejected (or a worker-batch digest mismatched)"
-
+        assert checks.get("ok_all_ranks", checks["ok"]), "honest workload rejected (or a digest mismatched): %r" % checks
     total_sigs = plan["total_sigs"] * args.steps       # every rank's signatures (node-wide)
     value = total_sigs / elapsed
 
-    iso = None
+    out = None
+    c2 = args.config == "C2"
+    cpu_inp = {}
     if rank == 0:
-        # k_verify alone (after the timed region, the GPU idle between launches): the timed launches
-        # run back to back (and, with batches in flight, beside the other batch's kernels), so their
-        # durations include the clock the chip holds under sustained load
-        eng.profile_enable(True)
-        for _ in range(3):
-            verify_step(streams[0], outs[0])
-            torch.cuda.synchronize()
-        eng.profile_enable(False)
-        iso = eng.profile_read()
-
-    if rank == 0:
-        avg_launch_s = (kms / kn) / 1e3 if kn else float("nan")
-        if ksigs is None:                              # library without nw_profile_read_sigs (A/B runs)
-            ksigs = cs.nsigs * kn
-        sigs_per_launch = ksigs / kn if kn else 0.0
-        kw = eng.key_window()
-        bw = eng.base_window()
-        fm = kverify_fm_per_sig(kw, bw)
-        peak = valu_peak_mad_per_s() / 1e12
-        achieved = sigs_per_launch * fm * MADS_PER_FM / avg_launch_s / 1e12
-        v1 = COST_MODEL_V1_FM.get(plan["votes"])
-        roofline = {
-            "bound": "valu", "kernel": "k_verify", "achieved": achieved, "peak": peak, "unit": "TMAD/s",
-            "frac": achieved / peak,
-            "traffic": traffic_per_launch() if args.config == "C2" else None,
-            "per_cycle": clock_frac_profile() if args.config == "C2" else None,
-            "avg_launch_ms": avg_launch_s * 1e3, "launches": kn,
-            "batches_in_flight": nst,
-            "isolated": None if not iso or not iso[1] else {
-                "avg_launch_ms": iso[0] / iso[1], "launches": iso[1],
-                "frac": sigs_per_launch * fm * MADS_PER_FM / (iso[0] / iso[1] / 1e3) / 1e12 / peak,
-                "note": "k_verify launched alone after the timed region, the GPU idle between launches (frac "
-                        "above: the timed launches, back to back%s)" % (
-                            ", overlapping the other batch's kernels" if nst > 1 else "")},
-            "work_model": "%.0f sigs/launch (%d launches per step) x %d FM/sig (7 FM per mixed addition x (%d basepoint "
-                          "+ %d key - 1) comb positions + 1 FM for the chain's first entry - 1 FM (no T in the last addition), key "
-                          "window %d) x 100 u32 "
-                          "MADs; SHA-512/mod-l/recoding VALU work not counted; peak = measured v_mad_u64_u32 rate"
-                          % (sigs_per_launch, kn // args.steps, fm, comb_pos(bw), comb_pos(kw), kw),
-            "dalek_equiv": {"fm_per_sig": v1, "TMADps": (sigs_per_launch * v1 * MADS_PER_FM / avg_launch_s / 1e12)
-                            if v1 else None,
-                            "note": "SURVEY §8(d) cost model v1 = dalek's MSM work per signature; the comb "
-                                    "algorithm needs %.1fx fewer FM" % (v1 / fm) if v1 else ""},
-        }
-        # single-certificate latency (H2D -> kernels -> D2H), the Core::run usage pattern
-        lat = []
-        for i in range(args.latency_samples):
-            c = i % cs.ncerts
-            f, n = int(cs.cert_first[c]), int(cs.cert_n[c])
-            t1 = time.perf_counter()
-            cok, _, _ = eng.verify_certs_np(np.array([0], np.uint32), np.array([n], np.uint32), cs.sigs[f:f + n],
-                                            slots[cs.signer[f:f + n]], cs.msgs[c:c + 1], zseed, first_cert + c)
-            lat.append(time.perf_counter() - t1)
-            assert cok[0] == 1
-        lat.sort()
-        strong = plan["scaling"] == "strong"
-        workload_desc = ("%s: %d-validator committee, %d certificates x %d votes (%d sigs) %s"
-                         % (args.config, plan["validators"], plan["node_certs"] if strong else plan["ncerts"],
-                            plan["votes"], plan["total_sigs"] if strong else cs.nsigs,
-                            "per node round, partitioned over the GPUs" if strong else "per GPU"))
-        if ndig:
-            workload_desc += " + %d worker-batch SHA-512 digests (%d B each) per GPU on a second stream" % (ndig, blen)
-            if from_host:
-                workload_desc += (", batches from pageable host memory (staged to pinned + H2D inside the timed "
-                                  "loop, double-buffered)")
+        iso = run.isolated()
+        roofline = run.roofline(iso, c2)
+        p50c, p99c = cert_latency(run, args.latency_samples)
         out = {
             "metric": METRIC, "value": value, "unit": "sigs/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": plan["scaling"], "vs_baseline": None, "dtype": "u32",
             "data": "synthetic (GPU-signed RFC 8032 signatures over SHA-512 certificate digests)",
-            "config": {"workload": workload_desc, "baseline_config": plan["baseline"],
-                       "validators": plan["validators"], "certs_per_gpu": cs.ncerts, "votes_per_cert": plan["votes"],
-                       "key_window": kw, "key_negtab": eng.key_negtab(),
+            "config": {"workload": run.workload_desc(), "baseline_config": plan["baseline"],
+                       "validators": plan["validators"], "certs_per_gpu": run.cs.ncerts,
+                       "votes_per_cert": plan["votes"], "key_window": run.eng.key_window(),
+                       "key_negtab": run.eng.key_negtab(),
                        "parallelism": "certificate shards per GPU; RCCL all_gather of verdict bitmaps + stake"},
-            "p50_cert_latency_ms": lat[len(lat) // 2] * 1e3 if lat else None,
-            "p99_cert_latency_ms": lat[int(len(lat) * 0.99)] * 1e3 if lat else None,
-            "roofline": roofline,
+            "p50_cert_latency_ms": p50c, "p99_cert_latency_ms": p99c,
+            "roofline": roofline, "checks": checks, "build": _lib.version(),
         }
-        if ndig:
-            out["digest_in_step"] = {"batches_per_gpu": ndig, "bytes_per_gpu_per_step": ndig * blen,
-                                     "GBps_per_gpu": ndig * blen * args.steps / elapsed / 1e9,
-                                     "batches_from_host": from_host}
-            if from_host:
-                out["digest_in_step"]["upload"] = uploader.stats()
+        if run.ndig:
+            out["digest_in_step"] = run.digest_in_step()
         # GPU legs first: the CPU baselines run more threads than the container's CPU quota, and the
         # cgroup throttling that follows would slow the host side of the next leg
-        c2 = args.config == "C2"
         if world == 1 and c2 and not args.no_extras:
-            out["host_fed"] = host_fed(eng, cs, slots, zseed)
-            out["msm"] = msm_leg(eng)
-            out["worker_digest"] = worker_digest_leg(eng)
+            out["host_fed"] = host_fed(run.eng, run.cs, run.slots, run.zseed)
+            out["msm"] = msm_leg(run.eng)
+            out["worker_digest"] = worker_digest_leg(run.eng)
             if args.latency_samples > 0:
-                out["latency"] = latency_legs(eng, com, slots, cs, args.latency_samples)
+                out["latency"] = latency_legs(run.eng, run.com, run.slots, run.cs, args.latency_samples, keep=cpu_inp)
         if world == 1 and c2 and args.digest_batches > 0:
-            out["digest"] = digest_leg(eng, dev, args.digest_batches, args.digest_share, 3,
-                                       0.0 if args.no_cpu_baseline else 3.0, verify_step)
+            out["digest"] = digest_leg(run.eng, run.dev, args.digest_batches, args.digest_share, 3, 0.0,
+                                       run.verify_step)
+    # the north-star config (configs[3]) in the same run, after the C2 engine is closed: one GPU's
+    # share of a 10,000-validator node round (1,250 certificates x 6,667 votes + 1,250 host-resident
+    # worker batches), at every world size
+    c4run = None
+    if c2 and args.c4_steps > 0:
+        run.close()
+        c4run = ConfigRun(leg_args(args, "C4"), world, rank, local)
+        el4, ch4 = c4run.run(args.c4_steps, args.c4_warmup)
+        if not args.timing_only:
+            assert ch4.get("ok_all_ranks", ch4["ok"]), "C4 leg: honest workload rejected or digest mismatch: %r" % ch4
+        if rank == 0:
+            out["c4"] = c4_block(c4run, el4, ch4, c4run.isolated())
+    if rank == 0:
         if not args.no_cpu_baseline:
             # every line carries the host baseline, N > 1 included: rank 0 times it after the timed
             # region while the other ranks block in a gloo barrier (a socket wait, no spinning host
             # thread to steal the cores being measured)
-            cb = cpu_baseline(cs, com, args.cpu_seconds, label=args.config)
-            if ndig:
-                cb["with_digests"] = cpu_step_with_digests(cb, host_b, plan, args.cpu_seconds / 3)
+            cb = cpu_baseline(run.cs, run.com, args.cpu_seconds, label=args.config)
+            if run.ndig:
+                cb["with_digests"] = cpu_step_with_digests(cb, run.host_b, plan, args.cpu_seconds / 3)
             cb["gpu_over_cpu"] = value / cb["value"]          # against the measured slice
             cb["gpu_over_host_extrapolated"] = value / cb["host_extrapolated"]["value"]   # against the whole host
             cb["ratios_note"] = ("gpu_over_cpu: this run's %d GPU(s) vs the measured %.0f-CPU slice; "
                                  "gpu_over_host_extrapolated: vs the whole host's %d physical cores (north star: "
                                  ">= 50x the host at 8 GPUs)" % (world, cb["measured_slice"]["cpus"],
                                                                   cb["host_extrapolated"]["physical_cores"]))
-            if ndig:
+            if run.ndig:
                 cb["with_digests"]["gpu_over_cpu"] = value / cb["with_digests"]["sigs_per_s"]
+            if cpu_inp:
+                lat = out["latency"]
+                wd = out.get("worker_digest", {}).get("one_batch_call_ms", {})
+                gpu = {"strict": (lat["strict_cached"]["p50_ms"], "latency.strict_cached"),
+                       "cert_67": (p50c, "p50_cert_latency_ms (nw_verify_certs, one C2 certificate)"),
+                       "cert_667": (lat["batch_cached_667"]["p50_ms"], "latency.batch_cached_667"),
+                       "cert_6667": (lat["batch_cached_6667"]["p50_ms"], "latency.batch_cached_6667"),
+                       "worker_batch": (wd.get("p50"), "worker_digest.one_batch_call_ms"),
+                       "header_6667_parents": (lat["header_digest_6667_parents"]["p50_ms"],
+                                               "latency.header_digest_6667_parents")}
+                cb["latency"] = cpu_latency(cpu_inp, gpu, args.cpu_latency_samples)
+                out["p50_cert_latency_cpu_ms"] = cb["latency"]["cert_67"]["p50_ms"]
             out["cpu_baseline"] = cb
+            if "digest" in out:
+                hb = c4run.host_b if c4run is not None else workload.worker_batches_np(256)
+                threads = max(cpu_thread_candidates())
+                bps, nb, dt = hashlib_rate(hb, threads, 3.0)
+                out["digest"]["cpu_baseline"] = {"GBps": bps / 1e9, "cores": threads,
+                                                 "kind": "hashlib (OpenSSL) SHA-512",
+                                                 "per_gpu_share_GBps": bps / 1e9 / GPUS_PER_NODE,
+                                                 "sample": "%d batches in %.1f s on %d threads" % (nb, dt, threads)}
+            if c4run is not None:
+                c4 = out["c4"]
+                threads = cb["measured_slice"]["threads"]
+                c4cb = cpu_baseline(c4run.cs, c4run.com, args.cpu_seconds / 2, label="C4", threads=threads)
+                c4cb["with_digests"] = cpu_step_with_digests(c4cb, c4run.host_b, c4run.plan, args.cpu_seconds / 5)
+                c4cb["gpu_over_cpu"] = c4["value"] / c4cb["with_digests"]["sigs_per_s"]
+                c4cb["gpu_over_host_extrapolated"] = c4["value"] / (
+                    c4cb["host_extrapolated"]["value"] * c4cb["with_digests"]["sigs_per_s"] / c4cb["value"])
+                c4cb["ratios_note"] = ("C4 step (verify + worker digests) on %d GPU(s) vs the same step done by the "
+                                       "measured %.0f-CPU slice (gpu_over_cpu) and by the whole host extrapolated "
+                                       "to its physical cores (north star: >= 50x the host at 8 GPUs)"
+                                       % (world, c4cb["measured_slice"]["cpus"]))
+                c4["cpu_baseline"] = c4cb
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

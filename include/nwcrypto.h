@@ -122,7 +122,9 @@ size_t nw_committee_size(const nw_ctx* ctx);
  * has not sized it yet). */
 int nw_key_window(const nw_ctx* ctx);
 /* 1 when every cached key table is stored with its negated copy (decided at the first load: when
- * twice the tables fit the HBM budget; NWCRYPTO_KEY_NEGTAB=0 disables), else 0.  Verdicts are the
+ * twice the tables fit the HBM budget of a committee-mode, declared-size (nw_opts.max_keys) or
+ * explicit-window context; never with an automatic window; the flag NW_OPT_NO_KEY_NEGTAB in
+ * nw_opts.flags disables it), else 0.  Verdicts are the
  * same either way; only k_verify's key pass differs (no conditional negation with the copies). */
 int nw_key_negtab(const nw_ctx* ctx);
 /* Basepoint comb window this library was built with (additions per s*B = ceil(256 / w)). */
@@ -254,7 +256,10 @@ int nw_sign_many_dev(nw_ctx* ctx, const uint8_t* d_seed32, const uint8_t* d_msgs
 
 /* ---- measurement --------------------------------------------------------------------------
  * When enabled, HIP events are recorded on the launch stream around every k_verify launch; read
- * back (synchronizing those events) the summed device time and launch count, then reset. */
+ * back (synchronizing those events) the summed device time and launch count, then reset.  Launches
+ * of at most 4,096 signatures run k_verify_split with k_finish's work fused into it (no separate
+ * k_finish launch): their samples cover verify + finish, so they are not comparable with large
+ * launches' samples (k_verify alone) or with builds before that fusion. */
 int nw_profile_enable(nw_ctx* ctx, int on);
 int nw_profile_read(nw_ctx* ctx, double* verify_ms_total, uint64_t* verify_launches);
 /* Same, plus the signatures covered by those launches (the roofline's work per launch). */

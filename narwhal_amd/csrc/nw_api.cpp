@@ -30,6 +30,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "nw_build_id.h"
 #include "nw_kernels.h"
 #include "nw_msm.h"
 #include "nw_point.h"
@@ -417,11 +418,12 @@ void fix_window(nw_ctx* ctx, size_t first_load) {
     // this context is sized for: k_verify's key pass then needs no conditional negation (7% of its
     // time at C2).  A large worker cache keeps the wider window instead (2 fewer comb positions are
     // worth more than the negation).  NW_OPT_NO_KEY_NEGTAB turns it off.
-    // (sized for: the declared max_keys, else the first load with committee mode's 25% headroom; an
-    // automatic window leaves room for 4x the first load)
-    const double sized = ctx->max_keys_user ? (double)std::max(ctx->max_keys, first_load)
-                                            : (double)first_load * (auto_window ? 4.0 : 1.25);
-    ctx->key_negtab = !(ctx->opt_flags & NW_OPT_NO_KEY_NEGTAB) &&
+    // Sized for: the declared max_keys, else the first load with 25% headroom (committee mode, or a
+    // window the caller chose).  An automatic window (nw_opts.key_window 0) is for callers that add
+    // keys over time with no declared bound: it never takes T-, whose doubled tables would halve the
+    // capacity max_keys allows below (the choice is permanent for the context).
+    const double sized = ctx->max_keys_user ? (double)std::max(ctx->max_keys, first_load) : (double)first_load * 1.25;
+    ctx->key_negtab = !(ctx->opt_flags & NW_OPT_NO_KEY_NEGTAB) && !auto_window &&
                       2.0 * sized * (double)comb_words(ctx->key_window) * 4.0 <= (double)budget;
     ctx->key_words = comb_words(ctx->key_window) * (ctx->key_negtab ? 2 : 1);
     ctx->key_reserve = ctx->max_keys_user && ctx->committee_mode;
@@ -730,7 +732,9 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
         }
     }
     NW_TRY(launch_verify(vp, msgmode, ctx->key_window, st), "k_verify");
-    if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");   // brackets k_verify alone
+    // brackets k_verify alone, or k_verify_split + the finish fused into it (split_fuses_finish:
+    // launches of <= 4,096 signatures; nwcrypto.h, nw_profile_read)
+    if (ev_stop) NW_TRY(hipEventRecord(ev_stop, st), "hipEventRecord");
     // small launches: k_verify_split has done k_finish's work itself (split_fuses_finish)
     if (!split_fuses_finish(vp.gn, vp.fk)) NW_TRY(launch_finish(vp, st), "k_finish");
     if (!batch_mode) return NW_OK;   // strict verdicts only (bytes written by k_finish): no certificate pass
@@ -1219,7 +1223,7 @@ bool zseed_ok(nw_ctx* ctx, const uint8_t* zseed) {
 
 extern "C" {
 
-const char* nw_version(void) { return "nwcrypto 0.3 gfx950 " __DATE__; }
+const char* nw_version(void) { return "nwcrypto 0.4 gfx950 src " NW_SRC_HASH " commit " NW_SRC_COMMIT; }
 
 int nw_abi_version(void) { return NW_ABI_VERSION; }
 

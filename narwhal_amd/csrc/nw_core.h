@@ -139,40 +139,6 @@ NW_HD void hram_generic(uint32_t out[16], const uint32_t R[8], const uint32_t A[
 
 // A table entry as gathered for a signed digit: (y-x)/2 and (y+x)/2 loaded in the order the sign
 // needs (swapped for a negative digit: -q = ((y-x)/2, (y+x)/2, -d x y)), d x y as stored.
-#if NW_PACKED_ENT
-// Packed: each element is two 16-B loads of its 8 canonical words (96 of the line's 128 bytes).
-struct ent_sw {
-    uint4 m0, m1, p0, p1, c0, c1;
-};
-
-NW_HD ent_sw load_ent_sw(const uint32_t* __restrict__ e, bool neg) {
-    ent_sw r;
-    const uint4* m = reinterpret_cast<const uint4*>(e + (neg ? ENT_YPX : ENT_YMX));   // pairs with Y - X
-    const uint4* p = reinterpret_cast<const uint4*>(e + (neg ? ENT_YMX : ENT_YPX));   // pairs with Y + X
-    const uint4* c = reinterpret_cast<const uint4*>(e + ENT_XY2D);
-    r.p0 = p[0];
-    r.p1 = p[1];
-    r.m0 = m[0];
-    r.m1 = m[1];
-    r.c0 = c[0];
-    r.c1 = c[1];
-    return r;
-}
-
-NW_HD fe fe_from_packed(const uint4& a, const uint4& b) {
-    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-    return fe_frombytes_w(w);
-}
-
-// ypx / ymx as loaded (swapped for a negative digit), xy2d as stored (its sign: ge_madd_sgn)
-NW_HD ge_precomp ent_sw_precomp(const ent_sw& e) {
-    ge_precomp q;
-    q.ymx = fe_from_packed(e.m0, e.m1);
-    q.ypx = fe_from_packed(e.p0, e.p1);
-    q.xy2d = fe_from_packed(e.c0, e.c1);
-    return q;
-}
-#else
 // Unpacked: each half is two 16-B loads and one 8-B load; the two pad words are never fetched.
 struct ent_sw {
     uint4 m0, m1, p0, p1, c1, c2;
@@ -215,7 +181,6 @@ NW_HD ge_precomp ent_sw_precomp(const ent_sw& e) {
     q.xy2d = c;
     return q;
 }
-#endif
 
 // The chain's first entry: the fully signed entry (d x y negated too) as an extended point.
 NW_HD ge_p3 ent_sw_first(const ent_sw& e, bool neg) {
@@ -268,7 +233,7 @@ NW_HD void comb_pass(ge_p3& P, uint32_t sc[8], const uint32_t* __restrict__ tab,
 }
 
 // comb_pass with the signed digits precomputed (dig[pos * stride], the lane's slot of a shared
-// array): the 8-word scalar and its carry are not live during the additions (k_verify, NW_DIG_LDS).
+// array): the 8-word scalar and its carry are not live during the additions (k_verify).
 // NT: the table is followed by its negated copy T- (tab + comb_words(W), k_comb_negate): a digit's
 // sign only picks the address, and the addition is the plain ge_madd (no swap, no f/g selects).
 // LAST: the chain's final addition computes X, Y, Z only (ge_madd_s2_xyz; P.T is left zero).
@@ -276,11 +241,7 @@ template <int W, bool FIRST, bool FUSED, bool NT = false, bool LAST = false>
 __device__ __forceinline__ void comb_pass_dig(ge_p3& P, const int* dig, int stride, const uint32_t* __restrict__ tab,
                                               bool neg_pos) {
     auto gather = [&](int pos, int d, bool ng) -> ent_sw {
-#ifdef NW_TIMING_HOT_ENTRIES   // timing-only variant builds (wrong verdicts): 16 L2-resident entries per position
-        const uint32_t* e = tab + ((size_t)pos * comb_ent(W) + ((d < 0 ? -d : d) & 15)) * PRECOMP_WORDS;
-#else
         const uint32_t* e = tab + ((size_t)pos * comb_ent(W) + (d < 0 ? -d : d)) * PRECOMP_WORDS;
-#endif
         if constexpr (NT) return load_ent_sw(e + (ng ? comb_words(W) : 0), false);
         else return load_ent_sw(e, ng);
     };

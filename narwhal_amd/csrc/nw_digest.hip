@@ -105,10 +105,6 @@ static constexpr uint32_t SPLIT_MAX_N = 32768;    // above: k_sha512_many (every
 // 160 KB; the workgroup's own 63,360 B + the pad leaves < 24 KB).  The price: such a workgroup
 // needs an EMPTY CU, which a running k_verify (its dispatcher refilling every freed slot) may not
 // leave until it drains, so a lone header's digest (one workgroup, latency-critical) stays unpadded.
-// NW_SHA_EXCLUSIVE=0: no pad (A/B variant builds).
-#ifndef NW_SHA_EXCLUSIVE
-#define NW_SHA_EXCLUSIVE 1
-#endif
 static constexpr uint32_t SHA_EXCLUSIVE_PAD = 80000;
 static constexpr uint32_t SHA_EXCLUSIVE_MIN_WG = 8;
 
@@ -306,7 +302,7 @@ hipError_t launch_sha512_many(uint32_t n, const uint8_t* base, const uint64_t* o
     if (n <= SPLIT_MAX_N) {
         const uint32_t blocks = blocks_for(n, SPLIT2_MSGS);
         uint32_t pad = 0;
-        if (NW_SHA_EXCLUSIVE) {
+        {
             static const int cus = [] {
                 int dev = 0, c = 0;
                 if (hipGetDevice(&dev) != hipSuccess ||

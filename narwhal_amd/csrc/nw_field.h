@@ -140,17 +140,8 @@ NW_HD fe fe_reduce_wide(uint64_t h[10]) {
 // picks for 2 * x at half rate (profiles/r01/isa/isa_rates_vop2.jsonl).  Off by default: it removes
 // 35 of 1,264 VALU instructions per comb step but measured no faster at C2 (k_verify 1.188 vs
 // 1.181 ms, profiles/r02/ab_r02d.txt) — the loop is bound by v_mad_u64_u32 issue, not by these.
-#ifndef NW_ADD_DBL
-#define NW_ADD_DBL 0
-#endif
 NW_HD uint32_t dbl32(uint32_t x) {
-#if defined(__HIP_DEVICE_COMPILE__) && NW_ADD_DBL
-    uint32_t r;
-    asm("v_add_u32 %0, %1, %1" : "=v"(r) : "v"(x));
-    return r;
-#else
     return 2u * x;
-#endif
 }
 
 // Fused-carry product scanning (the mixed addition's products, ge_madd).  Column k of h = f g is
@@ -476,7 +467,7 @@ NW_HD bool fe_eq(const fe& f, const fe& g) {
 // MI355X at C2 (profiles/r01_ab_select.txt): k_verify 1.214 ms vs 1.230 ms with cndmask selects.
 NW_HD uint32_t lane_mask(bool b) {
     uint32_t m = 0u - (uint32_t)b;
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(NW_CNDMASK_SELECT)
+#if defined(__HIP_DEVICE_COMPILE__)
     asm("" : "+v"(m));
 #endif
     return m;

@@ -344,11 +344,6 @@ __global__ void __launch_bounds__(64 * MSM_BUCKET_WAVES) k_msm_bucket(MsmParams 
     int32_t* s_hb = s_hb_w[wv];
     uint32_t* s_thru = s_thru_w[wv];
     const MsmTask task = a.tasks[tix];
-#ifdef NW_MSM_TIMING   // variant builds only (tools/build_variants.sh): per-phase shader cycles
-    uint64_t tst[5];
-    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
-    tst[0] = __builtin_amdgcn_s_memtime();
-#endif
     const size_t E = 2 * (size_t)a.nsig;
     const int16_t* dg = a.dig + (size_t)task.win * E + task.e0;
     const uint32_t m = task.e1 - task.e0;   // <= MSM_CH (host-checked)
@@ -360,9 +355,6 @@ __global__ void __launch_bounds__(64 * MSM_BUCKET_WAVES) k_msm_bucket(MsmParams 
         if (d) atomicAdd(&cur[(uint32_t)(d < 0 ? -d : d) - 1u], 1u);
     }
     wave_lds_sync();
-#ifdef NW_MSM_TIMING
-    tst[1] = __builtin_amdgcn_s_memtime();
-#endif
     // 2. exclusive scan: lane L owns buckets [L SPL, L SPL + SPL)
     uint32_t loc[SPL];
     uint32_t sum = 0;
@@ -396,9 +388,6 @@ __global__ void __launch_bounds__(64 * MSM_BUCKET_WAVES) k_msm_bucket(MsmParams 
         }
     }
     wave_lds_sync();
-#ifdef NW_MSM_TIMING
-    tst[2] = __builtin_amdgcn_s_memtime();
-#endif
     // 4. balanced accumulation: lane L takes sorted positions [p0, p1)
     const uint32_t q = (total + 63) / 64;
     const uint32_t p0 = min(total, L * q), p1 = min(total, p0 + q);
@@ -449,9 +438,6 @@ __global__ void __launch_bounds__(64 * MSM_BUCKET_WAVES) k_msm_bucket(MsmParams 
     s_hb[L] = hb;
     s_thru[L] = thru;
     wave_lds_sync();
-#ifdef NW_MSM_TIMING
-    tst[3] = __builtin_amdgcn_s_memtime();
-#endif
     // 5. merge runs that cross slice boundaries: the lane holding a bucket's first entry adds the
     //    head partials of the following lanes (through-partials continue the chain)
     if (tb >= 0) {
@@ -494,14 +480,6 @@ __global__ void __launch_bounds__(64 * MSM_BUCKET_WAVES) k_msm_bucket(MsmParams 
         X = ge_add_p3(X, V);   // lanes >= off add garbage; only lane 0's result is used
     }
     if (L == 0) store_p3(a.wpart + (size_t)task.out * MSM_PT_WORDS, X);
-#ifdef NW_MSM_TIMING
-    tst[4] = __builtin_amdgcn_s_memtime();
-    if (L == 0 && (tix % 16) == 0)
-        printf("MSMT %u %u %u %llu %llu %llu %llu %llu %u\n", tix, task.win, task.e1 - task.e0,
-               (unsigned long long)rt0, (unsigned long long)(tst[1] - tst[0]), (unsigned long long)(tst[2] - tst[1]),
-               (unsigned long long)(tst[3] - tst[2]), (unsigned long long)(tst[4] - tst[3]),
-               __builtin_amdgcn_s_getreg((31 << 11) | 4));
-#endif
 }
 
 // One wave per (batch, window): sum of the window's chunk partials into slot wfirst[bw].

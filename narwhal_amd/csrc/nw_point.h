@@ -32,22 +32,12 @@ struct ge_cached {
 // to the product T d x y instead, ge_madd_sgn, or taken from the negated copy of the table,
 // k_comb_negate).  Round 4's layout ([0..9] [10..19] [20..29], pad) needed the entry whole before
 // 30 selects.
-// NW_PACKED_ENT=1 (variant builds): [0..7] (y+x)/2, [8..15] (y-x)/2, [16..23] d x y as canonical
+// A packed variant (round 5): [0..7] (y+x)/2, [8..15] (y-x)/2, [16..23] d x y as canonical
 // 255-bit words, [24..31] unused: a gather touches 96 of the 128 bytes and unpacks the limbs after
 // the load (fe_frombytes_w, ~46 VALU per comb step).  Measured at C2 (profiles/r05/kverify_ab_r05.txt):
 // k_verify 1.092-1.113 ms packed vs 1.093-1.119 ms unpacked, i.e. no gain for 4% more VALU per
 // wave, so the unpacked layout stays the default.
-#ifndef NW_PACKED_ENT
-#define NW_PACKED_ENT 0
-#endif
-#if NW_PACKED_ENT
-static constexpr int ENT_YPX = 0, ENT_YMX = 8, ENT_XY2D = 16;
-#else
 static constexpr int ENT_YPX = 0, ENT_YMX = 12, ENT_XY2D = 22;
-#endif
-#ifndef NW_HALF_NIELS
-#define NW_HALF_NIELS 1
-#endif
 static constexpr int PRECOMP_WORDS = 32;
 // Fixed-base combs: signed radix-2^W digits, one table per digit position holding the multiples
 // |d| * 2^(W*pos) * P for |d| = 0..2^(W-1) (0 = identity).  W = 24 for the basepoint (11 positions,
@@ -82,21 +72,15 @@ NW_HD ge_p3 ge_identity() {
 
 NW_HD ge_precomp ge_precomp_identity() {
     ge_precomp r;
-#if NW_HALF_NIELS
     r.ypx = fe_from_const(FE_HALF);
     r.ymx = fe_from_const(FE_HALF);
-#else
-    r.ypx = fe_one();
-    r.ymx = fe_one();
-#endif
     r.xy2d = fe_zero();
     return r;
 }
 
 #ifndef NW_MADD3
-#define NW_MADD3 1   // with NW_DIG_LDS (k_verify): a, b, c as one three-way fused group
+#define NW_MADD3 1   // with the digits in LDS (k_verify): a, b, c as one three-way fused group
 #endif
-#if NW_HALF_NIELS
 // p + q (mixed, halved entry).  The HWCD formulas with every quantity halved: A/2 = (Y1-X1)(y-x)/2,
 // B/2, C/2 = T1 d x y, D/2 = Z1 (no doubling), E/2, F/2 = Z1 - C/2, G/2, H/2; the products
 // E F, G H, G F, E H are the sum times 1/4 in every coordinate, i.e. the same projective point.
@@ -185,14 +169,8 @@ NW_HD madd_mid ge_madd_s1_sgn(const ge_p3& p, const ge_precomp& q, uint32_t m) {
     r.e = fe_sub_loose(b, a);
     r.h = fe_add(b, a);
     const fe fq = fe_sub2p_loose(p.Z, c), gq = fe_add(p.Z, c);
-#ifdef NW_TIMING_NO_FG_SELECT   // timing-only variant builds (wrong verdicts)
-    (void)m;
-    r.f = fq;
-    r.g = gq;
-#else
     r.f = fe_select_mask(fq, gq, m);
     r.g = fe_select_mask(gq, fq, m);
-#endif
     return r;
 }
 
@@ -238,54 +216,14 @@ NW_HD ge_p3 ge_from_precomp(const ge_precomp& q) {
     r.T = fe_mul(q.xy2d, fe_from_const(FE_INVD));
     return r;
 }
-#else
-// p + q (mixed).  Limb budget: (Y1+X1) k=2, D = 2Z1 k=2, G = D + C k=3, xy2d may be k=2 (negated).
-// (Y1-X1) and e = b - a skip the carry pass (fe_sub_loose, k = 5): each only ever feeds fe_mul as
-// the first operand against a second operand of k <= 2 (ymx tight; f tight; h k=2): 5 x 2 <= 32.
-template <bool FUSED = false>
-NW_HD ge_p3 ge_madd(const ge_p3& p, const ge_precomp& q) {
-    const fe a = fe_mul(fe_sub_loose(p.Y, p.X), q.ymx);
-    const fe b = fe_mul(fe_add(p.Y, p.X), q.ypx);
-    const fe c = fe_mul(p.T, q.xy2d);
-    const fe d = fe_add(p.Z, p.Z);
-    const fe e = fe_sub_loose(b, a);
-    const fe h = fe_add(b, a);
-    const fe f = fe_sub(d, c);
-    const fe g = fe_add(d, c);
-    ge_p3 r;
-    r.X = fe_mul(e, f);
-    r.Y = fe_mul(g, h);
-    r.Z = fe_mul(g, f);
-    r.T = fe_mul(e, h);
-    return r;
-}
 
-// X = (y+x) - (y-x) = 2x, Y = 2y, Z = 2, T = 2xy = (2dxy) / d.
-NW_HD ge_p3 ge_from_precomp(const ge_precomp& q) {
-    ge_p3 r;
-    r.X = fe_sub(q.ypx, q.ymx);
-    r.Y = fe_carry(fe_add(q.ypx, q.ymx));
-    r.Z = fe_zero();
-    r.Z.v[0] = 2;
-    r.T = fe_mul(q.xy2d, fe_from_const(FE_INVD));
-    return r;
-}
-#endif
-
-// Table-entry form of affine (x, y) (tight limbs): halved affine Niels, or plain when
-// NW_HALF_NIELS is 0.
+// Table-entry form of affine (x, y) (tight limbs): halved affine Niels.
 NW_HD ge_precomp ge_precomp_from_affine(const fe& x, const fe& y) {
     ge_precomp q;
-#if NW_HALF_NIELS
     const fe half = fe_from_const(FE_HALF);
     q.ypx = fe_mul(fe_add(y, x), half);
     q.ymx = fe_mul(fe_sub(y, x), half);
     q.xy2d = fe_mul(fe_mul(x, y), fe_from_const(FE_D));
-#else
-    q.ypx = fe_carry(fe_add(y, x));
-    q.ymx = fe_sub(y, x);
-    q.xy2d = fe_mul(fe_mul(x, y), fe_from_const(FE_D2));
-#endif
     return q;
 }
 
@@ -415,9 +353,6 @@ NW_HD bool y_is_small_order(const uint32_t yw[8]) {
 
 // Conditionally negate an affine Niels entry: -(x, y) = (-x, y) swaps y+x / y-x and negates 2dxy.
 NW_HD ge_precomp ge_precomp_cneg(const ge_precomp& q, bool neg) {
-#ifdef NW_TIMING_NO_CNEG   // timing-only variant builds (wrong verdicts): the cost of the negation
-    return q;
-#endif
     ge_precomp r = q;
     const uint32_t m = lane_mask(neg);
     fe_cswap_mask(r.ypx, r.ymx, m);
@@ -427,30 +362,17 @@ NW_HD ge_precomp ge_precomp_cneg(const ge_precomp& q, bool neg) {
 
 NW_HD ge_precomp ge_precomp_from_words(const uint32_t* w) {
     ge_precomp q;
-#if NW_PACKED_ENT
-    q.ypx = fe_frombytes_w(w + ENT_YPX);
-    q.ymx = fe_frombytes_w(w + ENT_YMX);
-    q.xy2d = fe_frombytes_w(w + ENT_XY2D);
-#else
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
         q.ypx.v[i] = w[ENT_YPX + i];
         q.ymx.v[i] = w[ENT_YMX + i];
         q.xy2d.v[i] = w[ENT_XY2D + i];
     }
-#endif
     return q;
 }
 
 // The 32 words of a table entry (the layout above).
 NW_HD void precomp_to_words(const ge_precomp& q, uint32_t* w) {
-#if NW_PACKED_ENT
-    fe_tobytes_w(w + ENT_YPX, q.ypx);
-    fe_tobytes_w(w + ENT_YMX, q.ymx);
-    fe_tobytes_w(w + ENT_XY2D, q.xy2d);
-#pragma unroll
-    for (int i = 24; i < 32; ++i) w[i] = 0;
-#else
 #pragma unroll
     for (int i = 0; i < 10; ++i) {
         w[ENT_YPX + i] = q.ypx.v[i];
@@ -459,7 +381,6 @@ NW_HD void precomp_to_words(const ge_precomp& q, uint32_t* w) {
     }
     w[10] = 0;
     w[11] = 0;
-#endif
 }
 
 // Table-entry (halved affine Niels) form of p (one inversion); tight limbs.

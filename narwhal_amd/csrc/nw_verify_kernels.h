@@ -61,9 +61,6 @@ __device__ __forceinline__ uint32_t park_mismatch(const VerifyParams& a, uint32_
 // Occupancy: the 32-byte-digest kernel (certificates, votes, headers: the hot path) is held to
 // 168 VGPRs = 3 waves per SIMD (a few spills, measured faster than 2 waves at 169-175 VGPRs).
 // The generic-message kernel (worker chunks) is left unbounded: bounding it spills heavily.
-#ifndef NW_DIG_LDS
-#define NW_DIG_LDS 1   // digits precomputed into LDS (0: consumed from the scalar in the loop)
-#endif
 #ifndef NW_VERIFY_WAVES
 #define NW_VERIFY_WAVES 3
 #endif
@@ -89,7 +86,6 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     }
     uint32_t* frow = a.pbuf + (size_t)PREC_FLAGS_ROW * a.n;
     frow[gid] = flags;   // parked (coalesced) so neither flags nor i stays live through the combs
-#if NW_DIG_LDS
     // every signed digit of s and h computed up front into LDS: neither scalar nor the digit carry
     // is live during the comb additions (register room for a three-product first group, NW_MADD3)
     constexpr int NB = comb_pos(B_WINDOW), NA = comb_pos(WA);
@@ -109,11 +105,6 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     comb_pass_dig<B_WINDOW, true, MSGMODE == 0 && NW_MADD_FUSED, B_NEGTAB>(P, digs + threadIdx.x, 256, a.btab, false);
     comb_pass_dig<WA, false, MSGMODE == 0 && NW_MADD_FUSED, NT, true>(P, digs + NB * 256 + threadIdx.x, 256,
                                                                a.key_tab + (size_t)slot * a.key_stride, true);
-#else
-    // fused-carry products only in the 3-waves-per-SIMD kernel (MSGMODE 0); see ge_madd_s1
-    const ge_p3 P = compute_P<WA, B_WINDOW, MSGMODE == 0 && NW_MADD_FUSED>(S, h, sok, a.btab,
-                                                                           a.key_tab + (size_t)slot * a.key_stride);
-#endif
     // X, Z and the partial flags (y match, R sign, R small) in processing order, struct-of-arrays
     // (column gid): coalesced for k_finish, which completes the flags and writes flags[i].  R, i
     // and flags are re-read here rather than kept live through the combs (10 VGPRs): that keeps
@@ -122,7 +113,7 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     asm volatile("" ::: "memory");
     const uint32_t i2 = a.perm ? a.perm[gid] : gid;
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i2 * 16);
-    store_prec_soa(a.pbuf, a.n, gid, P, park_mismatch<!NW_DIG_LDS>(a, i2, P, verify_pflags(P, R, frow[gid])));
+    store_prec_soa(a.pbuf, a.n, gid, P, park_mismatch<false>(a, i2, P, verify_pflags(P, R, frow[gid])));
 }
 
 // Latency-mode kernel for small launches (nw_verify_split.h, compiled in nw_kvs.hip).
@@ -142,9 +133,6 @@ hipError_t launch_split_wa(const VerifyParams& p, int msgmode, hipStream_t st);
 // (bid, nb): this workgroup's index among the nb workgroups that share the list.
 template <int MSGMODE, int WA>
 __device__ __forceinline__ void slow_prep(const VerifyParams& a, uint32_t bid, uint32_t nb) {
-#ifdef NW_SLOW_TIMING
-    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
-#endif
     const uint32_t cnt = *a.slow_count;
     // Entries are dealt to the blocks first (entry t -> block t mod grid, thread t / grid): the few
     // thousand entries of an adversarial batch land on wave 0 of every block, one working wave per
@@ -171,9 +159,6 @@ __device__ __forceinline__ void slow_prep(const VerifyParams& a, uint32_t bid, u
         }
         uint32_t R[8];
         load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
-#ifdef NW_SLOW_TIMING   // variant builds only (tools/build_variants.sh): per-phase shader cycles
-        const uint64_t tm0 = __builtin_amdgcn_s_memtime();
-#endif
         ge_p3 Rp;
         if (!ge_decompress(Rp, R)) {
             if (owner) {
@@ -183,9 +168,6 @@ __device__ __forceinline__ void slow_prep(const VerifyParams& a, uint32_t bid, u
             }
             continue;
         }
-#ifdef NW_SLOW_TIMING
-        const uint64_t tm1 = __builtin_amdgcn_s_memtime();
-#endif
         ge_p3 P;
         if (fi & NW_F_P_SAVED) {
             P = load_p3(a.pslow + (size_t)i * 40);
@@ -194,23 +176,12 @@ __device__ __forceinline__ void slow_prep(const VerifyParams& a, uint32_t bid, u
             lane_inputs<MSGMODE>(a, i, R2, S, slot, kinfo, c2, h);
             P = compute_P<WA>(S, h, true, a.btab, a.key_tab + (size_t)slot * a.key_stride);
         }
-#ifdef NW_SLOW_TIMING
-        const uint64_t tm2 = __builtin_amdgcn_s_memtime();
-#endif
         const ge_p3 D = ge_add(Rp, ge_cached_neg(ge_to_cached(P)));
         uint32_t z4[4];
         coeff_z(a, i, cert, z4);
         const bool zzero = (z4[0] | z4[1] | z4[2] | z4[3]) == 0;
         const ge_p3 D2 = ge_dbl(D), D4 = ge_dbl(D2);
         const bool small = ge_is_identity(ge_dbl(D4));
-#ifdef NW_SLOW_TIMING
-        const uint64_t tm3 = __builtin_amdgcn_s_memtime();
-        if (owner)
-            printf("slow_prep t=%u saved=%d dec=%llu P=%llu Dz8=%llu small=%d rt0=%llu rt1=%llu\n", t,
-                   (fi & NW_F_P_SAVED) ? 1 : 0, (unsigned long long)(tm1 - tm0), (unsigned long long)(tm2 - tm1),
-                   (unsigned long long)(tm3 - tm2), small ? 1 : 0, (unsigned long long)rt_start,
-                   (unsigned long long)__builtin_amdgcn_s_memrealtime());
-#endif
         const uint32_t kind = (small || zzero) ? SK_SMALL : SK_BIG;
         if (kind == SK_BIG) {
             if (owner) {

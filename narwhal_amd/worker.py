@@ -65,9 +65,11 @@ def worker_engine(device: int = -1, processors: int = PROCESSORS_PER_WORKER, key
 
 def batch_tx_count(batch) -> int:
     """Transactions in a serialized ``WorkerMessage`` (bincode 1.3: u32 LE variant; ``Batch`` =
-    u64 LE count, then each transaction as u64 LE length + bytes).  Returns -1 for another variant
-    (``BatchRequest``: the reference's ``if let WorkerMessage::Batch`` does not verify it).  A
-    malformed message raises ValueError where the reference's ``deserialize(..).unwrap()`` panics
+    u64 LE count, then each transaction as u64 LE length + bytes).  Returns -1 for a well-formed
+    ``BatchRequest(Vec<Digest>, PublicKey)`` (worker/src/worker.rs:37-40: u64 LE count, that many
+    32-byte digests, then the key as its base64 string, u64 LE length + bytes, crypto/src/lib.rs:94-112;
+    the reference's ``if let WorkerMessage::Batch`` does not verify it).  A malformed message of
+    either variant raises ValueError where the reference's ``deserialize(..).unwrap()`` panics
     (processor.rs:68)."""
     mv = memoryview(batch).cast("B")
     if len(mv) < 4:
@@ -75,6 +77,7 @@ def batch_tx_count(batch) -> int:
     (variant,) = struct.unpack_from("<I", mv, 0)
     if variant != WORKER_MSG_BATCH:
         if variant == 1:
+            _check_batch_request(mv)
             return -1
         raise ValueError("WorkerMessage: unknown variant %d" % variant)
     if len(mv) < 12:
@@ -89,6 +92,23 @@ def batch_tx_count(batch) -> int:
         if pos > len(mv):
             raise ValueError("WorkerMessage::Batch: truncated transaction")
     return n
+
+
+def _check_batch_request(mv) -> None:
+    """bincode ``WorkerMessage::BatchRequest(Vec<Digest>, PublicKey)`` after its variant word."""
+    from .primary import _b64_decode
+    if len(mv) < 12:
+        raise ValueError("WorkerMessage::BatchRequest: truncated digest count")
+    (n,) = struct.unpack_from("<Q", mv, 4)
+    pos = 12 + 32 * n
+    if pos + 8 > len(mv):
+        raise ValueError("WorkerMessage::BatchRequest: truncated digests or key length")
+    (ln,) = struct.unpack_from("<Q", mv, pos)
+    if pos + 8 + ln > len(mv):
+        raise ValueError("WorkerMessage::BatchRequest: truncated public key")
+    raw = _b64_decode(bytes(mv[pos + 8:pos + 8 + ln]))
+    if raw is None or len(raw) < 32:
+        raise ValueError("WorkerMessage::BatchRequest: bad base64 public key")
 
 
 def sim_chunks(count: int):

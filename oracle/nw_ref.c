@@ -76,7 +76,25 @@ static fe51 fe_mul(fe51 a, fe51 b) {
     r.v[0] &= MASK51;
     return r;
 }
-static fe51 fe_sq(fe51 a) { return fe_mul(a, a); }
+/* dedicated squaring, 15 products (dalek FieldElement51::pow2k) */
+static fe51 fe_sq(fe51 a) {
+    const uint64_t a3_19 = a.v[3] * 19, a4_19 = a.v[4] * 19;
+    u128 c0 = (u128)a.v[0] * a.v[0] + 2 * ((u128)a.v[1] * a4_19 + (u128)a.v[2] * a3_19);
+    u128 c1 = (u128)a.v[3] * a3_19 + 2 * ((u128)a.v[0] * a.v[1] + (u128)a.v[2] * a4_19);
+    u128 c2 = (u128)a.v[1] * a.v[1] + 2 * ((u128)a.v[0] * a.v[2] + (u128)a.v[4] * a3_19);
+    u128 c3 = (u128)a.v[4] * a4_19 + 2 * ((u128)a.v[0] * a.v[3] + (u128)a.v[1] * a.v[2]);
+    u128 c4 = (u128)a.v[2] * a.v[2] + 2 * ((u128)a.v[0] * a.v[4] + (u128)a.v[1] * a.v[3]);
+    fe51 r;
+    c1 += (uint64_t)(c0 >> 51); r.v[0] = (uint64_t)c0 & MASK51;
+    c2 += (uint64_t)(c1 >> 51); r.v[1] = (uint64_t)c1 & MASK51;
+    c3 += (uint64_t)(c2 >> 51); r.v[2] = (uint64_t)c2 & MASK51;
+    c4 += (uint64_t)(c3 >> 51); r.v[3] = (uint64_t)c3 & MASK51;
+    uint64_t carry = (uint64_t)(c4 >> 51); r.v[4] = (uint64_t)c4 & MASK51;
+    r.v[0] += carry * 19;
+    r.v[1] += r.v[0] >> 51;
+    r.v[0] &= MASK51;
+    return r;
+}
 static fe51 fe_sqn(fe51 a, int n) {
     for (int i = 0; i < n; ++i) a = fe_sq(a);
     return a;
@@ -618,6 +636,8 @@ static void nwz(uint8_t z[32], const uint8_t key[32], uint32_t counter, uint64_t
 
 /* ------------------------------------------------------------------------------- API */
 static ge GE_B;
+typedef struct { fe51 YpX, YmX, XY2d; } ge_an;   /* affine Niels (dalek AffineNielsPoint) */
+static ge_an B_ODD[64];                            /* B, 3B, ..., 127B */
 static pthread_once_t init_once = PTHREAD_ONCE_INIT;
 
 static void init_consts(void) {
@@ -635,6 +655,17 @@ static void init_consts(void) {
     fe_reduce(&FE_D2);
     FE_SQRTM1 = fe_from_bytes(sqrtm1_bytes);
     ge_decompress(&GE_B, b_bytes);
+    {
+        ge b2 = ge_dbl(&GE_B), cur = GE_B;
+        for (int i = 0; i < 64; ++i) {
+            fe51 zi = fe_invert(cur.Z);
+            fe51 x = fe_mul(cur.X, zi), y = fe_mul(cur.Y, zi);
+            B_ODD[i].YpX = fe_add(y, x);
+            B_ODD[i].YmX = fe_sub(y, x);
+            B_ODD[i].XY2d = fe_mul(fe_mul(x, y), FE_D2);
+            cur = ge_add(&cur, &b2);
+        }
+    }
     memcpy(L_BYTES, SC_L32, 32);
 }
 
@@ -654,8 +685,68 @@ int nwr_decompress(const uint8_t in[32], uint8_t out_canonical[32]) {
     return 1;
 }
 
-/* dalek PublicKey::verify_strict (vartime double-base: NAF5 for -A, NAF8-style via the same
- * Straus machinery for B; the result point is algorithm-independent) */
+/* dalek PublicKey::verify_strict.  R = [k](-A) + [s]B by dalek's serial
+ * vartime_double_base::mul (curve25519-dalek 3.x, the precomputed-tables default): width-5 NAF of k
+ * over a per-call projective Niels table of -A, width-8 NAF of s over the precomputed affine Niels
+ * odd multiples of B (AFFINE_ODD_MULTIPLES_OF_BASEPOINT), the loop starting at the highest nonzero
+ * digit of either.  The result point is algorithm-independent; the shape matters for the latency
+ * comparator (bench.py cpu_baseline.latency). */
+static ge_c ge_add_an(const ge* p, const ge_an* q) {
+    fe51 ypx = fe_add(p->Y, p->X), ymx = fe_sub(p->Y, p->X);
+    fe51 pp = fe_mul(ypx, q->YpX), mm = fe_mul(ymx, q->YmX);
+    fe51 txy2d = fe_mul(p->T, q->XY2d);
+    fe51 z2 = fe_add(p->Z, p->Z);
+    ge_c r;
+    r.X = fe_sub(pp, mm);
+    r.Y = fe_add(pp, mm);
+    r.Z = fe_add(z2, txy2d);
+    r.T = fe_sub(z2, txy2d);
+    return r;
+}
+static ge_c ge_sub_an(const ge* p, const ge_an* q) {
+    fe51 ypx = fe_add(p->Y, p->X), ymx = fe_sub(p->Y, p->X);
+    fe51 pm = fe_mul(ypx, q->YmX), mp = fe_mul(ymx, q->YpX);
+    fe51 txy2d = fe_mul(p->T, q->XY2d);
+    fe51 z2 = fe_add(p->Z, p->Z);
+    ge_c r;
+    r.X = fe_sub(pm, mp);
+    r.Y = fe_add(pm, mp);
+    r.Z = fe_sub(z2, txy2d);
+    r.T = fe_add(z2, txy2d);
+    return r;
+}
+
+static ge double_base_vartime(const uint8_t a[32], const ge* A, const uint8_t b[32]) {
+    int8_t an[256], bn[256];
+    naf(an, a, 5);
+    naf(bn, b, 8);
+    int i = 255;
+    while (i > 0 && an[i] == 0 && bn[i] == 0) --i;
+    naf_table5 ta;
+    make_naf_table5(&ta, A);
+    ge r = ge_identity();
+    for (;; --i) {
+        ge_c t = ge_double_c(&r);
+        if (an[i] > 0) {
+            ge e = ge_from_c(&t);
+            t = ge_add_pn(&e, &ta.t[an[i] / 2]);
+        } else if (an[i] < 0) {
+            ge e = ge_from_c(&t);
+            t = ge_sub_pn(&e, &ta.t[(-an[i]) / 2]);
+        }
+        if (bn[i] > 0) {
+            ge e = ge_from_c(&t);
+            t = ge_add_an(&e, &B_ODD[bn[i] / 2]);
+        } else if (bn[i] < 0) {
+            ge e = ge_from_c(&t);
+            t = ge_sub_an(&e, &B_ODD[(-bn[i]) / 2]);
+        }
+        r = ge_from_c_proj(&t);
+        if (i == 0) break;
+    }
+    return r;   /* projective: ge_eq uses X, Y, Z only */
+}
+
 int nwr_verify_strict(const uint8_t* msg, size_t len, const uint8_t pk[32], const uint8_t sig[64]) {
     nwr_init();
     if (!sc_canonical(sig + 32)) return 0;
@@ -669,13 +760,7 @@ int nwr_verify_strict(const uint8_t* msg, size_t len, const uint8_t pk[32], cons
     ge mA = A;
     mA.X = fe_neg(A.X);
     mA.T = fe_neg(A.T);
-    uint8_t sc[2][32];
-    memcpy(sc[0], k, 32);
-    memcpy(sc[1], sig + 32, 32);
-    ge pts[2] = {mA, GE_B};
-    int8_t nafs[512];
-    naf_table5 tabs[2];
-    ge Rp = msm_straus((const uint8_t(*)[32])sc, pts, 2, nafs, tabs);
+    ge Rp = double_base_vartime(k, &mA, sig + 32);
     return ge_eq(&Rp, &R);
 }
 

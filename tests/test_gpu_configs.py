@@ -359,7 +359,7 @@ def nw_ref_sign_other(com, cs, i):
 
 
 # ----------------------------------------------------------------------------- C4
-def test_c4_w12_sample_vs_oracle_and_localized():
+def test_c4_w13_every_certificate_vs_oracle_and_localized():
     eng = _engine()
     try:
         com, slots, cs = _setup(eng, 10000, 1250, 6667)

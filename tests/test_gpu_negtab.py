@@ -108,3 +108,27 @@ def test_shared_basepoint_table_outlives_the_first_context(workload_200):
     finally:
         e2.close()
         e1.close()
+
+
+def test_auto_window_never_takes_negated_copies(workload_200):
+    """an automatic window (nw_opts.key_window 0: keys added over time, no declared
+    bound) keeps single tables, so its key capacity is not halved by T-; an explicit window on the same
+    keys takes T- (2.9 GB of W12 tables).  Verdicts on both equal the oracle's (the workload's
+    corrupted votes)."""
+    from narwhal_amd import _lib
+    com, cs, sigs, bad = workload_200
+    sel = slice(0, 64)
+    first = np.asarray(cs.cert_first[sel], np.uint32)
+    n = np.asarray(cs.cert_n[sel], np.uint32)
+    nsig = int(first[-1] + n[-1])
+    want = np.ones(len(n), bool)
+    want[sorted({int(b) // VOTES for b in bad if b < nsig})] = False
+    for window, negtab in ((0, False), (12, True)):
+        eng = _lib.Engine(device=0, key_window=window)
+        try:
+            s = np.asarray(eng.committee_load_np(com.pks, com.stake), np.uint32)
+            assert eng.key_negtab() == negtab, (window, eng.key_window())
+            ok, _, _ = eng.verify_certs_np(first, n, sigs[:nsig], s[cs.signer[:nsig]], cs.msgs[sel], ZSEED, 0)
+            assert (ok.astype(bool) == want).all()
+        finally:
+            eng.close()

@@ -135,10 +135,16 @@ def test_batch_tx_count_parses_worker_messages():
     assert w.batch_tx_count(workload.worker_batch(977, 512)) == 977
     assert w.batch_tx_count(workload.worker_batch(0, 512)) == 0
     assert w.batch_tx_count(workload.worker_batch(5, 9)) == 5
-    req = struct.pack("<IQ", 1, 0) + struct.pack("<Q", 32) + b"k" * 32   # BatchRequest(vec![], origin)
+    import base64
+    key = base64.b64encode(bytes(range(32)))                            # PublicKey: its base64 string
+    req = struct.pack("<IQ", 1, 2) + bytes(64) + struct.pack("<Q", len(key)) + key   # BatchRequest(2 digests, origin)
     assert w.batch_tx_count(req) == -1
+    assert w.batch_tx_count(struct.pack("<IQ", 1, 0) + struct.pack("<Q", len(key)) + key) == -1
+    short = base64.b64encode(bytes(24))                                 # decodes to < 32 bytes
     good = workload.worker_batch(3, 16)
-    for bad in (good[:-1], good[:10], b"\x02\0\0\0", b""):
+    for bad in (good[:-1], good[:10], b"\x02\0\0\0", b"", req[:-1], req[:40], req[:12],
+                struct.pack("<IQ", 1, 0) + struct.pack("<Q", len(short)) + short,
+                struct.pack("<IQ", 1, 0) + struct.pack("<Q", 4) + b"!!!!"):
         with pytest.raises(ValueError):
             w.batch_tx_count(bad)
 
