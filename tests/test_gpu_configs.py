@@ -429,6 +429,37 @@ def test_sha512_many_mixed_lengths_unaligned(engine):
     assert not bad, [(i, lens[i]) for i in bad[:10]]
 
 
+def test_sha512_many_33_groups_mixed_lengths(engine):
+    """k_sha512_split2 on 33 groups of 32 messages (an exclusive-CU launch: >= 8 workgroups) with mixed
+    lengths, so the groups end after different block counts and one group is partial; unaligned
+    offsets; vs hashlib.  (Round 6 A/B'd two groups per workgroup on this shape: rejected,
+    profiles/r06/c4_digest_packing_ab_r06.txt.)"""
+    import torch
+    rng = np.random.default_rng(23)
+    n = 32 * 32 + 5
+    lens = [0, 1, 111, 112, 127, 128, 129, 239, 240, 255, 256, 5000] + \
+        [int(x) for x in rng.integers(0, 9000, size=n - 13)] + [70001]
+    msgs = [rng.integers(0, 256, size=k, dtype=np.uint8).tobytes() for k in lens]
+    offs, pos = [], 5
+    for m in msgs:
+        offs.append(pos)
+        pos += len(m) + int(rng.integers(0, 5))
+    blob = np.zeros(pos + 16, np.uint8)
+    for o, m in zip(offs, msgs):
+        blob[o:o + len(m)] = np.frombuffer(m, np.uint8)
+    dev = torch.device("cuda", 0)
+    d_blob = torch.from_numpy(blob).to(dev)
+    d_off = torch.tensor(offs, dtype=torch.int64, device=dev)
+    d_len = torch.tensor(lens, dtype=torch.int64, device=dev)
+    d_out = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
+    engine.sha512_many_dev(d_blob.data_ptr(), d_off.data_ptr(), d_len.data_ptr(), n, d_out.data_ptr(),
+                           torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    got = d_out.cpu().numpy()
+    bad = [i for i, m in enumerate(msgs) if bytes(got[i]) != hashlib.sha512(m).digest()]
+    assert not bad, [(i, lens[i]) for i in bad[:10]]
+
+
 # ----------------------------------------------------------------------------- C4 headers
 def test_c4_headers_with_6667_parents():
     """(f)2 at the size that motivates it: at N = 10,000 a header carries 2f+1 = 6,667 parents, so
