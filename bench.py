@@ -792,6 +792,19 @@ def latency_legs(eng, com, slots, cs, samples, keep=None):
         f, n = int(c_cs.cert_first[c]), int(c_cs.cert_n[c])
         keep["certs"][n] = (bytes(c_cs.msgs[c]), [bytes(c_com.pks[k]) for k in c_cs.signer[f:f + n]],
                             [bytes(x) for x in c_cs.sigs[f:f + n]])
+
+    # n header / vote checks in ONE call (CoreBatcher's batching, core.py): the crossover against n
+    # one-at-a-time CPU checks (cpu_latency strict_xN)
+    keep["strict_many"] = {}
+    for nm in (2, 8, 64):
+        sel = [(k * 67) % cs.nsigs for k in range(nm)]
+        m_msgs = [bytes(cs.msgs[int(np.searchsorted(cs.cert_first, j, side="right")) - 1]) for j in sel]
+        m_pks = [bytes(com.pks[cs.signer[j]]) for j in sel]
+        m_sigs = [bytes(cs.sigs[j]) for j in sel]
+        mcall = eng.prepare_strict_many_call(m_msgs, m_pks, m_sigs)
+        assert all(mcall())
+        out["strict_cached_x%d" % nm] = p50(mcall, samples)
+        keep["strict_many"][nm] = list(zip(m_msgs, m_pks, m_sigs))
     fseed = np.frombuffer(os.urandom(32), np.uint8).reshape(1, 32)
     fpk, fsig = eng.sign_many_np(fseed, np.frombuffer(msg, np.uint8).reshape(1, 32))
     fpk, fsig = bytes(fpk[0]), bytes(fsig[0])
@@ -1240,6 +1253,10 @@ def cpu_latency(inp, gpu, samples=100):
     msg, pk, sig = inp["strict"]
     assert nw_ref.verify_strict(pk, msg, sig)
     out["strict"] = stats(lambda: nw_ref.verify_strict(pk, msg, sig), 2 * samples)
+    for nm, triples in sorted(inp.get("strict_many", {}).items()):
+        assert all(nw_ref.verify_strict(p_, m_, s_) for m_, p_, s_ in triples)
+        out["strict_x%d" % nm] = stats(lambda: [nw_ref.verify_strict(p_, m_, s_) for m_, p_, s_ in triples],
+                                       max(20, samples // max(1, nm // 8)))
     zseed = bytes(32)
     for votes, (digest, pks, sigs) in sorted(inp["certs"].items()):
         call = nw_ref.prepare_crypto_verify_batch(digest, pks, sigs)
@@ -1363,6 +1380,8 @@ def main(argv=None):
                 lat = out["latency"]
                 wd = out.get("worker_digest", {}).get("one_batch_call_ms", {})
                 gpu = {"strict": (lat["strict_cached"]["p50_ms"], "latency.strict_cached"),
+                       **{"strict_x%d" % nm: (lat["strict_cached_x%d" % nm]["p50_ms"], "latency.strict_cached_x%d" % nm)
+                          for nm in (2, 8, 64) if "strict_cached_x%d" % nm in lat},
                        "cert_67": (p50c, "p50_cert_latency_ms (nw_verify_certs, one C2 certificate)"),
                        "cert_667": (lat["batch_cached_667"]["p50_ms"], "latency.batch_cached_667"),
                        "cert_6667": (lat["batch_cached_6667"]["p50_ms"], "latency.batch_cached_6667"),

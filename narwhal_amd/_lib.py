@@ -210,6 +210,20 @@ class Engine:
                                              _buf(b"".join(map(bytes, sigs))), n, ok), "nw_verify_strict_many")
         return [bool(x) for x in ok]
 
+    def prepare_strict_many_call(self, msgs, pks, sigs):
+        """nw_verify_strict_many with the arguments marshalled once (latency measurement: the call
+        alone is timed, as a Rust caller passes its slices): returns call() -> ctypes uint8 array."""
+        n = len(sigs)
+        mp = (ctypes.c_char_p * n)(*[bytes(m) for m in msgs])
+        ln = (ctypes.c_size_t * n)(*[len(m) for m in msgs])
+        pk_blob, sig_blob = b"".join(map(bytes, pks)), b"".join(map(bytes, sigs))
+        ok = (ctypes.c_uint8 * n)()
+
+        def call():
+            self.check(LIB.nw_verify_strict_many(self._ctx, mp, ln, pk_blob, sig_blob, n, ok), "nw_verify_strict_many")
+            return ok
+        return call
+
     def verify_batch(self, msgs, pks, sigs, zseed: bytes, batch_index: int = 0) -> bool:
         n = len(sigs)
         if len(msgs) != n or len(pks) != n:

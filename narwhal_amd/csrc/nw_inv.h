@@ -248,6 +248,50 @@ NW_HD fe fe_invert_var(const fe& z) {
     return s30_to_fe(d);
 }
 
+#if defined(__HIPCC__)
+// ---- one inversion per wave, on the scalar unit ------------------------------------------------
+// A lone lane's inversion is a serial chain of ~14 k VALU instructions that a wave issues at ~6-7
+// cycles each when nothing hides the latency (k_finish's one wave per SIMD, a single header check).
+// The same safegcd on WAVE-UNIFORM operands compiles to scalar (SALU) code, whose dependent
+// instructions issue back to back: z is taken from the first active lane (readfirstlane) and every
+// operation below is on uniform values.  Callers batch their lanes' values into one uniform product
+// first (fe_invert_batched).
+__device__ __forceinline__ fe fe_invert_wave(const fe& z_in) {
+    fe z;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) z.v[k] = (uint32_t)__builtin_amdgcn_readfirstlane((int)z_in.v[k]);
+    return fe_invert_var(z);
+}
+
+__device__ __forceinline__ fe fe_shfl_xor(const fe& x, int off) {
+    fe r;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) r.v[k] = (uint32_t)__shfl_xor((int)x.v[k], off, 64);
+    return r;
+}
+
+// z^-1 for every lane of the wave, where lanes [g*GS, g*GS + GS) all hold the same z (GS lanes per
+// value; every lane of the wave active): Montgomery's trick over the wave's 64 / GS values by an
+// xor butterfly (log2(64 / GS) levels of two products: the running product, identical in every lane
+// at the end since each level multiplies the same pair in both partners, and the product of the
+// OTHER values), one scalar-unit inversion of the wave's product, one product back.  A zero z
+// contributes 1 and gets 0 (as fe_invert_var(0)).
+template <int GS>
+__device__ __forceinline__ fe fe_invert_batched(const fe& z) {
+    const bool zz = fe_iszero(z);
+    fe t = fe_select(z, fe_one(), zz);
+    fe others = fe_one();
+#pragma unroll
+    for (int off = GS; off < 64; off <<= 1) {
+        const fe p = fe_shfl_xor(t, off);
+        others = fe_mul(others, p);
+        t = fe_mul(t, p);
+    }
+    const fe r = fe_mul(fe_invert_wave(t), others);
+    return fe_select(r, fe_zero(), zz);
+}
+#endif
+
 // z^-1 mod p (0 -> 0), same result as fe_invert.
 NW_HD fe fe_invert_sg(const fe& z) {
     uint32_t w[8];

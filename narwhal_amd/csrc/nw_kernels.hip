@@ -122,14 +122,18 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
 // ONE (a.fk == 1: finish_k_for gives it to launches of up to 256 x 4 x 64 = 262,144 signatures,
 // i.e. every latency-bound call and mid-size batches up to one lane per SIMD slot): its own kernel,
 // so the chunked path's register allocation is untouched.
+// Above this many signatures k_finish inverts per lane (more than 8 waves per CU would queue on the
+// CUs' scalar units); at or below, one scalar-unit inversion per wave.
+static constexpr uint32_t FINISH_SALU_MAX_SIGS = 1u << 21;
+
 template <bool ONE>
 __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
     const uint32_t NL = (a.gn + a.fk - 1) / a.fk;
     const uint32_t Lr = blockIdx.x * blockDim.x + threadIdx.x;
-    // fewer lanes than a wave (one header or vote signature: ONE inversion on one lane): the idle
-    // lanes of wave 0 run duplicates (no writes), since a wave with a sparse EXEC mask issues its
-    // chain 1.2-1.4x slower
-    if (Lr >= NL && (NL >= 64 || Lr >= 64)) return;
+    // a wave with any owned lane keeps all 64: the lanes past NL run duplicates (no writes), for the
+    // wave-batched inversion (every lane of the wave takes part) and because a wave with a sparse
+    // EXEC mask issues its chain 1.2-1.4x slower
+    if ((Lr & ~63u) >= NL) return;
     const bool owner = Lr < NL;
     const uint32_t L = owner ? Lr : Lr % NL;
     const uint32_t cnt = (a.gn - L + NL - 1) / NL;   // columns g0 + L + k NL < g0 + gn  (cnt <= fk)
@@ -142,7 +146,8 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
         const fe X = load_fe_soa(a.pbuf, n, gbase);
         const uint32_t pf = a.pbuf[PREC_FLAGS_ROW * n + gbase];
         const uint32_t i = a.perm ? a.perm[gbase] : (uint32_t)gbase;
-        const fe zi = (NW_INV_VAR && a.gn <= 8) ? fe_invert_var(z) : fe_invert_sg(z);
+        // the wave's lanes share one scalar-unit inversion (ONE: <= 65,536 signatures, <= 4 waves per CU)
+        const fe zi = fe_invert_batched<1>(z);
         const uint32_t f = finish_x_flags(X, zi, pf);
         if (owner) emit(i, pf, f);
         return;
@@ -160,16 +165,12 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
                 store_fe_soa(a.pre, n, g, acc);   // duplicates store the owner's own values (scratch)
             }
         }
-        // Inversion: variable-time safegcd (public data) when each lane chains several signatures
-        // (throughput-bound launches: fewer instructions on average); the branch-free constant-time
-        // divsteps for one signature per lane (latency-bound launches: with 64 independent inversions
-        // per wave the variable-time loop runs the slowest lane's count, measured 10% slower there:
-        // profiles/r02/ab_r02.txt).  a.fk is uniform, so the branch does not diverge.
-        // A launch of a handful of signatures (one header / vote signature) has a handful of active
-        // lanes, so the variable-time loop's cost is that one lane's own count: variable time again.
-        fe inv;
-        if (NW_INV_VAR && (a.fk >= 4 || a.gn <= 8)) inv = fe_invert_var(acc);
-        else inv = fe_invert_sg(acc);
+        // Inversion: the wave's 64 chain products share ONE variable-time safegcd (public data) on
+        // the scalar unit (fe_invert_batched: a 6-level butterfly of products, nw_inv.h); round 5 ran
+        // one per lane on the VALU, half of the kernel's ~29 k VALU instructions per wave.  A CU's
+        // waves share its scalar unit, so launches of more than FINISH_SALU_MAX_SIGS (C4: 32 waves
+        // per CU) keep the per-lane VALU inversion.  a.gn is uniform: the branch does not diverge.
+        fe inv = a.gn <= FINISH_SALU_MAX_SIGS ? fe_invert_batched<1>(acc) : fe_invert_var(acc);
 #pragma unroll
         for (int k = FINISH_K - 1; k >= 0; --k) {
             if ((uint32_t)k < cnt) {

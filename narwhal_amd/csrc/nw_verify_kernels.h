@@ -64,6 +64,9 @@ __device__ __forceinline__ uint32_t park_mismatch(const VerifyParams& a, uint32_
 #ifndef NW_VERIFY_WAVES
 #define NW_VERIFY_WAVES 3
 #endif
+#ifndef NW_RSAVE_LDS
+#define NW_RSAVE_LDS 0   // 1: R and i parked in LDS at the start instead of re-read from HBM after the combs (A/B)
+#endif
 // NT: the key tables carry their negated copies (VerifyParams::key_negtab); the basepoint's does when
 // B_NEGTAB.
 template <int MSGMODE, int WA, bool NT>
@@ -90,6 +93,11 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     // is live during the comb additions (register room for a three-product first group, NW_MADD3)
     constexpr int NB = comb_pos(B_WINDOW), NA = comb_pos(WA);
     __shared__ int digs[(NB + NA) * 256];
+#if NW_RSAVE_LDS
+    __shared__ uint32_t rsave[8 * 256];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) rsave[k * 256 + threadIdx.x] = R[k];
+#endif
     {
         uint32_t sc[8];
         int carry = 0;
@@ -111,8 +119,14 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     // the kernel at <= 168 VGPRs = 3 waves per SIMD.  The compiler barrier stops the re-reads from
     // being merged with the first loads.
     asm volatile("" ::: "memory");
+#if NW_RSAVE_LDS
+    const uint32_t i2 = a.perm ? a.perm[gid] : gid;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) R[k] = rsave[k * 256 + threadIdx.x];
+#else
     const uint32_t i2 = a.perm ? a.perm[gid] : gid;
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i2 * 16);
+#endif
     store_prec_soa(a.pbuf, a.n, gid, P, park_mismatch<false>(a, i2, P, verify_pflags(P, R, frow[gid])));
 }
 

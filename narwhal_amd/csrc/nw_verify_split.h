@@ -69,7 +69,9 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
     // vote) runs duplicate groups on the rest of wave 0 (no writes): a wave with a sparse EXEC mask
     // issues its chain 1.2-1.4x slower.
     const uint32_t s_raw = t / VERIFY_SPLIT;
-    if (s_raw >= a.gn && (a.gn * VERIFY_SPLIT >= 64 || t >= 64)) return;
+    // FUSE: a wave with any signature keeps all its lanes (duplicates past the launch's last group)
+    // for the wave-batched inversion, which needs every lane of the wave
+    if (s_raw >= a.gn && (FUSE ? (t & ~63u) >= a.gn * VERIFY_SPLIT : (a.gn * VERIFY_SPLIT >= 64 || t >= 64))) return;
     const bool owner = s_raw < a.gn;
     const uint32_t gid = a.g0 + (owner ? s_raw : s_raw % a.gn);
     const uint32_t i = a.perm ? a.perm[gid] : gid;
@@ -146,7 +148,8 @@ __global__ void __launch_bounds__(256) k_verify_split(VerifyParams a) {
         const bool emits = j == 0 && owner;   // the group's writer (the other lanes: same chain, no stores)
         uint32_t pf = verify_pflags(P, R, flags);
         if (emits) pf = park_mismatch(a, i, P, pf);
-        const fe zi = (NW_INV_VAR && a.gn <= 8) ? fe_invert_var(P.Z) : fe_invert_sg(P.Z);
+        // the wave's 8 signature groups share ONE inversion, on the scalar unit (nw_inv.h)
+        const fe zi = fe_invert_batched<VERIFY_SPLIT>(P.Z);
         const uint32_t f = finish_x_flags(P.X, zi, pf);
         if (emits) finish_emit(a, i, pf, f);
         return;

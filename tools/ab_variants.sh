@@ -3,7 +3,7 @@
 set -o pipefail
 OUT=gpurun_out/${1:-ab}
 mkdir -p $OUT
-ARGS="--steps 20 --warmup 3 --no-cpu-baseline --digest-batches 0 --latency-samples 0 --no-extras ${BENCH_ARGS:-}"
+ARGS="--steps 20 --warmup 3 --c4-steps 0 --no-cpu-baseline --digest-batches 0 --latency-samples 0 --no-extras ${BENCH_ARGS:-}"
 for rep in 1 2; do
 for lib in default build_exp/*.so; do
   name=$(basename $lib .so)

@@ -7,7 +7,7 @@ RE=${2:-k_verify|k_finish|k_sha512}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
-CMD=${PMC_CMD:-"python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --latency-samples 0 ${BENCH_ARGS:-}"}
+CMD=${PMC_CMD:-"python3 bench.py --steps 2 --warmup 1 --c4-steps 0 --no-cpu-baseline --latency-samples 0 ${BENCH_ARGS:-}"}
 NPASS=${PMC_PASSES:-5}   # first N counter groups only
 i=0
 for ctrs in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU" \

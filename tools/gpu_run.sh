@@ -66,7 +66,7 @@ for step in "$@"; do
       summ "$OUT/bench_c4_$n.json" ;;
     prof_kv)
       timeout -k 10 "$(lim 400)" rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_kv" -o kv -- \
-        python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --latency-samples 0 --no-extras --digest-batches 0 \
+        python3 bench.py --steps 10 --warmup 2 --c4-steps 0 --no-cpu-baseline --latency-samples 0 --no-extras --digest-batches 0 \
         > "$OUT/bench_kv.json" 2> "$OUT/prof_kv.log" || die prof_kv "$OUT/prof_kv.log"
       python3 tools/roofline_rocprof.py "$OUT/prof_kv/kv_kernel_trace.csv" --bench "$OUT/bench_kv.json" --skip 2 \
         --take 10 > "$OUT/roofline_rocprof.json" && cat "$OUT/roofline_rocprof.json"

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 OUT=gpurun_out/${1:?usage: pmc_ab_r05.sh OUTTAG "tag [ENV=VAL ...]" ...}
 shift
 mkdir -p "$OUT"
-CMD="python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --latency-samples 0 --digest-batches 0 --no-extras"
+CMD="python3 bench.py --steps 4 --warmup 1 --c4-steps 0 --no-cpu-baseline --latency-samples 0 --digest-batches 0 --no-extras"
 for spec in "$@"; do
   set -- $spec
   tag=$1; shift
