@@ -64,9 +64,6 @@ __device__ __forceinline__ uint32_t park_mismatch(const VerifyParams& a, uint32_
 #ifndef NW_VERIFY_WAVES
 #define NW_VERIFY_WAVES 3
 #endif
-#ifndef NW_RSAVE_LDS
-#define NW_RSAVE_LDS 0   // 1: R and i parked in LDS at the start instead of re-read from HBM after the combs (A/B)
-#endif
 // NT: the key tables carry their negated copies (VerifyParams::key_negtab); the basepoint's does when
 // B_NEGTAB.
 template <int MSGMODE, int WA, bool NT>
@@ -93,11 +90,12 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     // is live during the comb additions (register room for a three-product first group, NW_MADD3)
     constexpr int NB = comb_pos(B_WINDOW), NA = comb_pos(WA);
     __shared__ int digs[(NB + NA) * 256];
-#if NW_RSAVE_LDS
+    // R parked in LDS for the y-match after the combs (not live through them, and not re-read from
+    // HBM: a scattered 32-B read that cost a line per signature; PMC cycles per C2 launch 2.04 ->
+    // 2.01 M, profiles/r06/pmc_rsave_r06.txt)
     __shared__ uint32_t rsave[8 * 256];
 #pragma unroll
     for (int k = 0; k < 8; ++k) rsave[k * 256 + threadIdx.x] = R[k];
-#endif
     {
         uint32_t sc[8];
         int carry = 0;
@@ -114,19 +112,14 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     comb_pass_dig<WA, false, MSGMODE == 0 && NW_MADD_FUSED, NT, true>(P, digs + NB * 256 + threadIdx.x, 256,
                                                                a.key_tab + (size_t)slot * a.key_stride, true);
     // X, Z and the partial flags (y match, R sign, R small) in processing order, struct-of-arrays
-    // (column gid): coalesced for k_finish, which completes the flags and writes flags[i].  R, i
-    // and flags are re-read here rather than kept live through the combs (10 VGPRs): that keeps
-    // the kernel at <= 168 VGPRs = 3 waves per SIMD.  The compiler barrier stops the re-reads from
-    // being merged with the first loads.
+    // (column gid): coalesced for k_finish, which completes the flags and writes flags[i].  R (from
+    // LDS), i and flags are re-read here rather than kept live through the combs (10 VGPRs): that
+    // keeps the kernel at <= 168 VGPRs = 3 waves per SIMD.  The compiler barrier stops the re-reads
+    // from being merged with the first loads.
     asm volatile("" ::: "memory");
-#if NW_RSAVE_LDS
     const uint32_t i2 = a.perm ? a.perm[gid] : gid;
 #pragma unroll
     for (int k = 0; k < 8; ++k) R[k] = rsave[k * 256 + threadIdx.x];
-#else
-    const uint32_t i2 = a.perm ? a.perm[gid] : gid;
-    load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i2 * 16);
-#endif
     store_prec_soa(a.pbuf, a.n, gid, P, park_mismatch<false>(a, i2, P, verify_pflags(P, R, frow[gid])));
 }
 
