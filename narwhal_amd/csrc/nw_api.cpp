@@ -133,7 +133,7 @@ struct Workspace {
     DevBuf w_sig, w_signer, w_keys, w_sig_cert, w_cert_first, w_cert_n, w_msg, w_msg_off, w_msg_len, w_flags,
         w_slow_count, w_slow_list, w_slow_slot, w_slow_buf, w_cert_ok, w_ok, w_misc, w_out, w_pbuf, w_pre, w_counts,
         w_cursor, w_perm, w_io, w_var, w_status, w_msm_ent, w_msm_dig, w_msm_zs, w_msm_meta, w_msm_bkt, w_msm_part,
-        w_msm_wpart, w_pslow, w_cert_state, w_exact;
+        w_msm_wpart, w_pslow, w_cert_state, w_exact, w_pinfo;
     HostBuf h_io, h_meta;
 
     // Grow a buffer; a buffer that may still be read by a pending call is only freed after it.
@@ -150,7 +150,7 @@ struct Workspace {
                           &w_msg_len, &w_flags, &w_slow_count, &w_slow_list, &w_slow_slot, &w_slow_buf, &w_cert_ok,
                           &w_ok, &w_misc, &w_out, &w_pbuf, &w_pre, &w_counts, &w_cursor, &w_perm, &w_io, &w_var,
                           &w_status, &w_msm_ent, &w_msm_dig, &w_msm_zs, &w_msm_meta, &w_msm_bkt, &w_msm_part,
-                          &w_msm_wpart, &w_pslow, &w_cert_state, &w_exact})
+                          &w_msm_wpart, &w_pslow, &w_cert_state, &w_exact, &w_pinfo})
             b->release();
         h_io.release();
         h_meta.release();
@@ -643,6 +643,7 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
         NW_TRY(ws->ensure(ws->w_counts, ctx->nkeys * 4 + 16), "ws counts");
         NW_TRY(ws->ensure(ws->w_cursor, ctx->nkeys * 4 + 16), "ws cursor");
         NW_TRY(ws->ensure(ws->w_perm, nsigs * 4 + 16), "ws perm");
+        NW_TRY(ws->ensure(ws->w_pinfo, nsigs * 8 + 16), "ws pinfo");
     }
     uint32_t* sig_cert = pre ? pre->sig_cert : ws->w_sig_cert.as<uint32_t>();
     uint32_t* slow_count = pre ? pre->zero4 : ws->w_slow_count.as<uint32_t>();
@@ -706,11 +707,14 @@ int enqueue_certs(nw_ctx* ctx, Workspace* ws, size_t ncerts, const uint32_t* d_f
     vp.pbuf = ws->w_pbuf.as<uint32_t>();
     vp.pre = ws->w_pre.as<uint32_t>();
     vp.perm = nullptr;
+    vp.pinfo = nullptr;
     if (group) {
-        NW_TRY(launch_group_scatter((uint32_t)nsigs, (uint32_t)ctx->nkeys, d_signer, ws->w_counts.as<uint32_t>(),
-                                    ws->w_cursor.as<uint32_t>(), ws->w_perm.as<uint32_t>(), st),
+        NW_TRY(launch_group_scatter((uint32_t)nsigs, (uint32_t)ctx->nkeys, d_signer, sig_cert,
+                                    ws->w_counts.as<uint32_t>(), ws->w_cursor.as<uint32_t>(), ws->w_perm.as<uint32_t>(),
+                                    ws->w_pinfo.as<uint2>(), st),
                "signer grouping");
         vp.perm = ws->w_perm.as<uint32_t>();
+        vp.pinfo = ws->w_pinfo.as<uint2>();
     }
     vp.g0 = 0;
     vp.gn = (uint32_t)nsigs;

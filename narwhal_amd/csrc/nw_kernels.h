@@ -81,6 +81,8 @@ struct VerifyParams {
     uint32_t* pbuf;                // [PREC_ROWS][n] SoA, processing order: P's X, Z + partial flags
     uint32_t* pre;                 // [10][n] SoA prefix products of Z (k_finish scratch)
     const uint32_t* perm;          // [n] processing order for k_verify (signer-grouped) or null
+    const uint2* pinfo;            // [n] with perm: (signer slot, sig_cert) of signature perm[g] at g, so
+                                   // k_verify reads them coalesced instead of two scattered 4-B loads
     uint32_t nkeys;                // key-cache slots (signer slots >= nkeys are rejected, never read)
     const uint32_t* sig_keys;      // k_verify_var: [n][8] raw key words of each signature (uncached keys)
 };
@@ -127,8 +129,9 @@ hipError_t launch_slow_tail(const VerifyParams& p, const FinalizeParams& f, int 
 hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, const uint32_t* first,
                               const uint32_t* nv, const uint32_t* signer, uint32_t* sig_cert, uint32_t* zero4,
                               uint32_t* counts, uint32_t* status, uint32_t* cert_state, hipStream_t st);
-hipError_t launch_group_scatter(uint32_t n, uint32_t nkeys, const uint32_t* signer, const uint32_t* counts,
-                                uint32_t* cursor, uint32_t* perm, hipStream_t st);
+hipError_t launch_group_scatter(uint32_t n, uint32_t nkeys, const uint32_t* signer, const uint32_t* sig_cert,
+                                const uint32_t* counts, uint32_t* cursor, uint32_t* perm, uint2* pinfo,
+                                hipStream_t st);
 hipError_t launch_flags_to_ok(uint32_t n, const uint32_t* flags, uint8_t* ok, hipStream_t st);
 // Tables for nk keys at tab + j * stride (u32 words); negtab: each followed by its negated copy
 // (stride >= 2 comb_words(window)).

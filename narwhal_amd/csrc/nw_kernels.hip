@@ -84,15 +84,22 @@ __global__ void __launch_bounds__(1024) k_scan_slots(uint32_t k, const uint32_t*
 }
 
 __global__ void __launch_bounds__(256) k_scatter_slots(uint32_t n, uint32_t nkeys, const uint32_t* signer,
-                                                       uint32_t* cursor, uint32_t* perm) {
+                                                       const uint32_t* sig_cert, uint32_t* cursor, uint32_t* perm,
+                                                       uint2* pinfo) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) perm[atomicAdd(&cursor[clamp_slot(signer[i], nkeys)], 1u)] = i;
+    if (i < n) {
+        const uint32_t s = signer[i];
+        const uint32_t g = atomicAdd(&cursor[clamp_slot(s, nkeys)], 1u);
+        perm[g] = i;
+        pinfo[g] = make_uint2(s, sig_cert[i]);
+    }
 }
 
 // Tile-local scatter: LDS histogram -> one global atomic per (tile, slot) reserves the tile's run
 // of each slot -> LDS atomics rank the tile's signatures inside their runs.
 __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t nkeys, const uint32_t* signer,
-                                                           uint32_t* cursor, uint32_t* perm) {
+                                                           const uint32_t* sig_cert, uint32_t* cursor, uint32_t* perm,
+                                                           uint2* pinfo) {
     extern __shared__ uint32_t lds[];
     uint32_t* base = lds;            // [nkeys] tile count, then the tile's global base
     uint32_t* rank = lds + nkeys;    // [nkeys] running rank inside the tile
@@ -109,8 +116,10 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
         if (base[k]) base[k] = atomicAdd(&cursor[k], base[k]);
     __syncthreads();
     for (uint32_t i = t0 + threadIdx.x; i < t1; i += blockDim.x) {
-        const uint32_t k = clamp_slot(signer[i], nkeys);
-        perm[base[k] + atomicAdd(&rank[k], 1u)] = i;
+        const uint32_t s = signer[i];
+        const uint32_t g = base[clamp_slot(s, nkeys)] + atomicAdd(&rank[clamp_slot(s, nkeys)], 1u);
+        perm[g] = i;
+        pinfo[g] = make_uint2(s, sig_cert[i]);   // the raw slot: k_verify does its own range check
     }
 }
 
@@ -391,16 +400,17 @@ hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, c
 }
 
 // Scan + scatter of the signer grouping whose counts k_expand_count produced.
-hipError_t launch_group_scatter(uint32_t n, uint32_t nkeys, const uint32_t* signer, const uint32_t* counts,
-                                uint32_t* cursor, uint32_t* perm, hipStream_t st) {
+hipError_t launch_group_scatter(uint32_t n, uint32_t nkeys, const uint32_t* signer, const uint32_t* sig_cert,
+                                const uint32_t* counts, uint32_t* cursor, uint32_t* perm, uint2* pinfo,
+                                hipStream_t st) {
     if (n == 0 || nkeys == 0) return hipSuccess;
     hipLaunchKernelGGL(k_scan_slots, dim3(1), dim3(1024), 0, st, nkeys, counts, cursor);
     if (nkeys <= GROUP_LDS_KEYS)
         hipLaunchKernelGGL(k_scatter_slots_lds, dim3(blocks_for(n, GROUP_TILE)), dim3(256), nkeys * 8, st, n, nkeys,
-                           signer, cursor, perm);
+                           signer, sig_cert, cursor, perm, pinfo);
     else
-        hipLaunchKernelGGL(k_scatter_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, nkeys, signer, cursor,
-                           perm);
+        hipLaunchKernelGGL(k_scatter_slots, dim3(blocks_for(n, 256)), dim3(256), 0, st, n, nkeys, signer, sig_cert,
+                           cursor, perm, pinfo);
     return hipGetLastError();
 }
 

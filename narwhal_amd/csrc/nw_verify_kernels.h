@@ -15,18 +15,23 @@ namespace nw {
 
 // Signature i's inputs and h = SHA-512(R || A || M) mod l.  cert is clamped to a valid index; the
 // returned bool says the signature lies in no certificate's range (NO_CERT: it gets no verdict).
-template <int MSGMODE>
+// PINFO (k_verify): the slot and certificate come from a.pinfo[gid] (processing order, coalesced) when
+// the launch has one; else from a.signer[i] / a.sig_cert[i].
+template <int MSGMODE, bool PINFO = false>
 __device__ __forceinline__ bool lane_inputs(const VerifyParams& a, uint32_t i, uint32_t R[8], uint32_t S[8],
-                                            uint32_t& slot, uint32_t& kinfo, uint32_t& cert, uint32_t h[8]) {
+                                            uint32_t& slot, uint32_t& kinfo, uint32_t& cert, uint32_t h[8],
+                                            uint32_t gid = 0) {
     uint32_t Aw[8];
+    uint2 sc = make_uint2(0u, 0u);
+    if (PINFO && a.pinfo) sc = a.pinfo[gid];
     load_w8(R, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16);
     load_w8(S, reinterpret_cast<const uint32_t*>(a.sig) + (size_t)i * 16 + 8);
-    slot = a.signer[i];
+    slot = (PINFO && a.pinfo) ? sc.x : a.signer[i];
     const bool in_cache = slot < a.nkeys;   // device inputs: an out-of-range slot is rejected
     slot = in_cache ? slot : 0u;
     load_w8(Aw, a.keys_raw + (size_t)slot * 8);
     kinfo = in_cache ? a.key_info[slot] : 0u;
-    cert = a.sig_cert[i];
+    cert = (PINFO && a.pinfo) ? sc.y : a.sig_cert[i];
     const bool nocert = cert == NO_CERT;   // a vote outside every range: k_finish gives it no verdict
     cert = nocert ? 0u : cert;
     if (MSGMODE == 0) {
@@ -73,7 +78,7 @@ __global__ void __launch_bounds__(256, MSGMODE == 0 ? NW_VERIFY_WAVES : 1) k_ver
     // signer-grouped order: the 64 lanes of a wave mostly share one key table (TLB / cache locality)
     const uint32_t i = a.perm ? a.perm[gid] : gid;
     uint32_t R[8], S[8], h[8], slot, kinfo, cert;
-    const bool nocert = lane_inputs<MSGMODE>(a, i, R, S, slot, kinfo, cert, h);
+    const bool nocert = lane_inputs<MSGMODE, true>(a, i, R, S, slot, kinfo, cert, h, gid);
     const bool sok = sc_is_canonical(S);
     const bool aok = (kinfo & KI_OK) != 0;
     uint32_t flags = (sok ? NW_F_S_OK : 0u) | (aok ? NW_F_A_OK : 0u) | ((kinfo & KI_SMALL) ? NW_F_A_SMALL : 0u) |
