@@ -131,10 +131,6 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
 // ONE (a.fk == 1: finish_k_for gives it to launches of up to 256 x 4 x 64 = 262,144 signatures,
 // i.e. every latency-bound call and mid-size batches up to one lane per SIMD slot): its own kernel,
 // so the chunked path's register allocation is untouched.
-// Above this many signatures k_finish inverts per lane (more than 8 waves per CU would queue on the
-// CUs' scalar units); at or below, one scalar-unit inversion per wave.
-static constexpr uint32_t FINISH_SALU_MAX_SIGS = 1u << 21;
-
 template <bool ONE>
 __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
     const uint32_t NL = (a.gn + a.fk - 1) / a.fk;
@@ -177,9 +173,9 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
         // Inversion: the wave's 64 chain products share ONE variable-time safegcd (public data) on
         // the scalar unit (fe_invert_batched: a 6-level butterfly of products, nw_inv.h); round 5 ran
         // one per lane on the VALU, half of the kernel's ~29 k VALU instructions per wave.  A CU's
-        // waves share its scalar unit, so launches of more than FINISH_SALU_MAX_SIGS (C4: 32 waves
-        // per CU) keep the per-lane VALU inversion.  a.gn is uniform: the branch does not diverge.
-        fe inv = a.gn <= FINISH_SALU_MAX_SIGS ? fe_invert_batched<1>(acc) : fe_invert_var(acc);
+        // waves share its scalar unit, but at 256 VGPRs this kernel runs one wave per SIMD, so at
+        // most four inversions (~12 k scalar instructions each) share it at a time.
+        fe inv = fe_invert_batched<1>(acc);
 #pragma unroll
         for (int k = FINISH_K - 1; k >= 0; --k) {
             if ((uint32_t)k < cnt) {
