@@ -20,19 +20,41 @@ int main(int argc, char** argv) {
             return 2;
         memset(h[k], k, per);
     }
-    auto run = [&](int L) {
+    // SPIN=1: wait by polling hipEventQuery on each stream's end event instead of hipDeviceSynchronize;
+    // the GPU-side span (first stream's start event -> each stream's end event) is printed beside the wall time
+    const bool spin = getenv("SPIN") && atoi(getenv("SPIN"));
+    std::vector<hipEvent_t> e0(8), e1(8);
+    for (int k = 0; k < 8; ++k)
+        if (hipEventCreate(&e0[k]) != hipSuccess || hipEventCreate(&e1[k]) != hipSuccess) return 3;
+    auto run = [&](int L, float& gpu_ms) {
         (void)hipDeviceSynchronize();
         auto t0 = std::chrono::steady_clock::now();
+        for (int k = 0; k < L; ++k) (void)hipEventRecord(e0[k], st[k]);
         for (size_t c = 0; c < npc; ++c)
             for (int k = 0; k < L; ++k)
                 (void)hipMemcpyAsync((char*)d[k] + c * piece, (char*)h[k] + c * piece, piece, hipMemcpyHostToDevice,
                                      st[k]);
-        (void)hipDeviceSynchronize();
-        return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3;
+        for (int k = 0; k < L; ++k) (void)hipEventRecord(e1[k], st[k]);
+        if (spin) {
+            for (int k = 0; k < L; ++k)
+                while (hipEventQuery(e1[k]) == hipErrorNotReady) {}
+        } else {
+            (void)hipDeviceSynchronize();
+        }
+        const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() * 1e3;
+        gpu_ms = 0;
+        for (int k = 0; k < L; ++k) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, e0[0], e1[k]);
+            gpu_ms = ms > gpu_ms ? ms : gpu_ms;
+        }
+        return wall;
     };
     for (int L : {1, 2, 4, 8}) {
-        const double a = run(L), b = run(L), c = run(L);
-        printf("streams %d x %zu KiB: first %.2f ms, second %.2f, third %.2f ms\n", L, per >> 10, a, b, c);
+        float ga, gb, gc;
+        const double a = run(L, ga), b = run(L, gb), c = run(L, gc);
+        printf("streams %d x %zu KiB: wall %.2f / %.2f / %.2f ms, GPU events %.2f / %.2f / %.2f ms%s\n", L, per >> 10, a, b,
+               c, ga, gb, gc, spin ? " (spin wait)" : "");
     }
     return 0;
 }
