@@ -217,11 +217,12 @@ def cpu_baseline(cs, com, seconds, probe_seconds=2.5, label="C2", threads=None):
             # threads beyond ~2x the quota only time-slice (profiles/r02/cpu_probe_r02.json)
             "cgroup_cpu_quota": cgroup_cpu_quota(), "affinity_cpus": host_cores(),
             "thread_sweep_sigs_per_s": sweep or None,
-            "sample": "%d certificates x %d votes of the %s workload (%d sigs) in %.1f s on %d threads (best of the "
-                      "sweep); oracle/nw_ref.c (C restatement of ed25519-dalek 1.0.1 u64 backend: per-vote A "
+            "sample": "%d certificates x %d votes of the %s workload (%d sigs) in %.1f s on %d threads (%s); "
+                      "oracle/nw_ref.c (C restatement of ed25519-dalek 1.0.1 u64 backend: per-vote A "
                       "decompression + Straus MSM below 190 votes, Pippenger above, as dalek's verify_batch via "
                       "crypto/src/lib.rs:206-219)"
-                      % (done_certs, int(cs.cert_n[0]), label, done_sigs, dt, threads)}
+                      % (done_certs, int(cs.cert_n[0]), label, done_sigs, dt, threads,
+                         "best of the sweep" if len(cands) > 1 else "thread count given")}
 
 
 def hashlib_rate(batches, threads, seconds):
