@@ -207,9 +207,12 @@ namespace {
 
 uint32_t finish_k_for(const nw_ctx* ctx, size_t n) {
     if (ctx->finish_k) return ctx->finish_k;
-    const size_t lanes = 256 * 4 * 64;
+    // k_finish<ONE> up to one lane per SIMD slot (256 CUs x 4 SIMDs x 64); above, the chunked kernel
+    // (four waves per SIMD) with the fewest signatures per lane that still fits the chip in one round
+    const size_t one_max = 256 * 4 * 64, lanes = one_max * 4;
+    if (n <= one_max) return 1;
     const size_t k = (n + lanes - 1) / lanes;
-    return k < 1 ? 1u : (k > (size_t)FINISH_K ? (uint32_t)FINISH_K : (uint32_t)k);
+    return k < 2 ? 2u : (k > (size_t)FINISH_K ? (uint32_t)FINISH_K : (uint32_t)k);
 }
 
 // Diagnostics are per calling thread (a context is shared by many threads).

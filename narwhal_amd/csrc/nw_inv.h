@@ -290,6 +290,51 @@ __device__ __forceinline__ fe fe_invert_batched(const fe& z) {
     const fe r = fe_mul(fe_invert_wave(t), others);
     return fe_select(r, fe_zero(), zz);
 }
+
+// z^-1 for every lane of a workgroup of NWAVES full waves (every thread of the block calls it, one
+// value per lane): the wave butterfly as above, then the NWAVES wave products meet in LDS and wave 0
+// runs the block's ONE scalar-unit inversion; slot is __shared__ scratch of (NWAVES + 1) x 10 words.
+// A CU's waves share one scalar unit, so with several waves per SIMD this cuts its work NWAVES-fold.
+template <int NWAVES>
+__device__ __forceinline__ fe fe_invert_block(const fe& z, uint32_t (*slot)[10]) {
+    const bool zz = fe_iszero(z);
+    fe t = fe_select(z, fe_one(), zz);
+    fe others = fe_one();
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const fe p = fe_shfl_xor(t, off);
+        others = fe_mul(others, p);
+        t = fe_mul(t, p);
+    }
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63u) == 0) {
+#pragma unroll
+        for (int k = 0; k < 10; ++k) slot[w][k] = t.v[k];
+    }
+    __syncthreads();
+    fe ow = fe_one();   // product of the other waves' products
+#pragma unroll
+    for (int v = 0; v < NWAVES; ++v) {
+        if ((uint32_t)v == w) continue;
+        fe tv;
+#pragma unroll
+        for (int k = 0; k < 10; ++k) tv.v[k] = slot[v][k];
+        ow = fe_mul(ow, tv);
+    }
+    if (w == 0) {
+        const fe inv = fe_invert_wave(fe_mul(ow, t));
+        if (threadIdx.x == 0) {
+#pragma unroll
+            for (int k = 0; k < 10; ++k) slot[NWAVES][k] = inv.v[k];
+        }
+    }
+    __syncthreads();
+    fe inv;
+#pragma unroll
+    for (int k = 0; k < 10; ++k) inv.v[k] = slot[NWAVES][k];
+    const fe r = fe_mul(fe_mul(inv, ow), others);
+    return fe_select(r, fe_zero(), zz);
+}
 #endif
 
 // z^-1 mod p (0 -> 0), same result as fe_invert.

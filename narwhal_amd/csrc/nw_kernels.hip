@@ -124,21 +124,26 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
 }
 
 // ------------------------------------------------------------------------------------ finish
-// Montgomery batch inversion of the Z of FINISH_K signatures per lane (one field inversion per
-// chunk), affine x, y, encoding match against R, strict verdict, and (batch mode) compaction of the
-// mismatching signatures into the exact-path list.  Lane L of NL owns the processing-order columns
-// g = L, L + NL, L + 2 NL, ... so every pbuf / pre access of a wave is one contiguous 256-B run.
-// ONE (a.fk == 1: finish_k_for gives it to launches of up to 256 x 4 x 64 = 262,144 signatures,
-// i.e. every latency-bound call and mid-size batches up to one lane per SIMD slot): its own kernel,
-// so the chunked path's register allocation is untouched.
+// Montgomery batch inversion of the Z of up to FINISH_K signatures per lane, affine x, y, encoding
+// match against R, strict verdict, and (batch mode) compaction of the mismatching signatures into
+// the exact-path list.  Lane L of NL owns the processing-order columns g = L, L + NL, L + 2 NL, ...
+// so every pbuf / pre access of a wave is one contiguous 256-B run.
+// ONE (a.fk == 1: finish_k_for gives it to launches of up to 256 x 4 x 64 = 65,536 signatures, i.e.
+// every latency-bound call, one wave per SIMD slot): no prefix products, one wave-batched inversion.
+// Chunked (fk >= 2): the two chains are plain loops (124 VGPRs, four waves per SIMD, the next
+// column's load issued one step ahead) and the workgroup's 256 lane products share ONE scalar-unit
+// inversion (fe_invert_block).  Round 6 first ran the chains fully unrolled with every load hoisted
+// (256 VGPRs, one wave per SIMD, a wave-batched inversion each): latency-bound, 1.17 ms per 8.3 M
+// signatures at C4 against 0.56 ms now, 126 against 104 us at C2 (profiles/r06/finish_ab_r06.txt).
 template <bool ONE>
 __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
     const uint32_t NL = (a.gn + a.fk - 1) / a.fk;
     const uint32_t Lr = blockIdx.x * blockDim.x + threadIdx.x;
-    // a wave with any owned lane keeps all 64: the lanes past NL run duplicates (no writes), for the
-    // wave-batched inversion (every lane of the wave takes part) and because a wave with a sparse
-    // EXEC mask issues its chain 1.2-1.4x slower
-    if ((Lr & ~63u) >= NL) return;
+    // A wave (ONE) or a workgroup (chunked: fe_invert_block synchronizes it) with any owned lane
+    // keeps all its lanes: the lanes past NL run duplicates (no writes), since every lane takes part
+    // in the batched inversion and a wave with a sparse EXEC mask issues its chain 1.2-1.4x slower
+    // (DESIGN.md §5.5).
+    if (ONE ? (Lr & ~63u) >= NL : blockIdx.x * blockDim.x >= NL) return;
     const bool owner = Lr < NL;
     const uint32_t L = owner ? Lr : Lr % NL;
     const uint32_t cnt = (a.gn - L + NL - 1) / NL;   // columns g0 + L + k NL < g0 + gn  (cnt <= fk)
@@ -155,41 +160,33 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
         const fe zi = fe_invert_batched<1>(z);
         const uint32_t f = finish_x_flags(X, zi, pf);
         if (owner) emit(i, pf, f);
-        return;
     } else {
-        // Both chains are fully unrolled over FINISH_K (guarded by cnt) so the column loads are
-        // independent of the running products and issue ahead of them: with one wave per SIMD the
-        // kernel is latency-bound, and a load inside the serial chain would stall it every step.
+        __shared__ uint32_t inv_slot[5][10];
         const uint32_t* zrow = a.pbuf + 10 * n;
         fe acc = fe_one();
-#pragma unroll
-        for (int k = 0; k < FINISH_K; ++k) {
-            if ((uint32_t)k < cnt) {
-                const size_t g = gbase + (size_t)k * NL;
-                acc = fe_mul(acc, load_fe_soa(zrow, n, g));
-                store_fe_soa(a.pre, n, g, acc);   // duplicates store the owner's own values (scratch)
-            }
+        fe znext = load_fe_soa(zrow, n, gbase);
+#pragma unroll 1
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const size_t g = gbase + (size_t)k * NL;
+            const fe z = znext;
+            if (k + 1 < cnt) znext = load_fe_soa(zrow, n, g + NL);
+            acc = fe_mul(acc, z);
+            // the last prefix is never read back; duplicates store the owner's own values (scratch)
+            if (k + 1 < cnt) store_fe_soa(a.pre, n, g, acc);
         }
-        // Inversion: the wave's 64 chain products share ONE variable-time safegcd (public data) on
-        // the scalar unit (fe_invert_batched: a 6-level butterfly of products, nw_inv.h); round 5 ran
-        // one per lane on the VALU, half of the kernel's ~29 k VALU instructions per wave.  A CU's
-        // waves share its scalar unit, but at 256 VGPRs this kernel runs one wave per SIMD, so at
-        // most four inversions (~12 k scalar instructions each) share it at a time.
-        fe inv = fe_invert_batched<1>(acc);
-#pragma unroll
-        for (int k = FINISH_K - 1; k >= 0; --k) {
-            if ((uint32_t)k < cnt) {
-                const size_t g = gbase + (size_t)k * NL;
-                fe zi = inv;
-                if (k > 0) {
-                    zi = fe_mul(inv, load_fe_soa(a.pre, n, g - NL));
-                    inv = fe_mul(inv, load_fe_soa(zrow, n, g));
-                }
-                const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
-                const uint32_t pf = a.pbuf[PREC_FLAGS_ROW * n + g];
-                const uint32_t f = finish_x_flags(load_fe_soa(a.pbuf, n, g), zi, pf);
-                if (owner) emit(i, pf, f);
+        fe inv = fe_invert_block<4>(acc, inv_slot);
+#pragma unroll 1
+        for (int k = (int)cnt - 1; k >= 0; --k) {
+            const size_t g = gbase + (size_t)k * NL;
+            fe zi = inv;
+            if (k > 0) {
+                zi = fe_mul(inv, load_fe_soa(a.pre, n, g - NL));
+                inv = fe_mul(inv, load_fe_soa(zrow, n, g));
             }
+            const uint32_t i = a.perm ? a.perm[g] : (uint32_t)g;
+            const uint32_t pf = a.pbuf[PREC_FLAGS_ROW * n + g];
+            const uint32_t f = finish_x_flags(load_fe_soa(a.pbuf, n, g), zi, pf);
+            if (owner) emit(i, pf, f);
         }
     }
 }
