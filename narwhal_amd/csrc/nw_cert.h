@@ -12,15 +12,22 @@
 namespace nw {
 
 // Per-certificate verdict: definitive Err on any bad S / undecodable A / undecodable R, else the
-// exact remaining batch sum (usually empty) must be the identity.  One 64-lane wave per
-// certificate: lanes stride over the votes (coalesced flag reads), wave reductions combine them;
-// the exact sum over slow-path terms (failing certificates only) is a lane-strided sum + shuffle tree.
-// One wave per certificate: flag reduction, stake sum, and the verdict whenever the flags decide it
-// (parse / decode failure, all votes matching, one term with a prime-order component).  The rest
-// (two or more slow-path terms) is appended to the exact list for k_cert_exact, which has the
-// registers for the point sum: this kernel stays at a handful of VGPRs and never spills.
-// Certificate c's finalize, by one wave (lane = 0..63).
-__device__ __forceinline__ void finalize_cert(const FinalizeParams& a, uint32_t c, uint32_t lane) {
+// exact remaining batch sum (usually empty) must be the identity.  The flag reduction, stake sum,
+// and the verdict whenever the flags decide it (parse / decode failure, all votes matching, one
+// term with a prime-order component) are the finalize; the rest (two or more slow-path terms) is
+// appended to the exact list for k_cert_exact, which has the registers for the point sum: the
+// finalize stays at a handful of VGPRs and never spills.  A certificate's votes are scanned by one
+// wave (finalize_cert) or, for large certificates, by a whole workgroup (k_cert_finalize_wg:
+// C4's 6,667 votes are 105 dependent load rounds for one wave, 7 for sixteen).
+struct FinalizeAcc {
+    bool bad, slow;
+    uint32_t tsum;
+    uint64_t stake;
+};
+
+// The votes t, t + stride, ... of certificate c (lanes stride over them: coalesced flag reads),
+// reduced over the calling wave: every lane returns the wave's totals.
+__device__ __forceinline__ FinalizeAcc finalize_scan(const FinalizeParams& a, uint32_t c, uint32_t t, uint32_t stride) {
     const uint32_t first = a.cert_first[c];
     // a vote range past the signature array (device inputs are not host-checked) rejects the
     // certificate; only the in-range votes are read
@@ -28,33 +35,35 @@ __device__ __forceinline__ void finalize_cert(const FinalizeParams& a, uint32_t 
     const uint32_t nv = range_bad ? (first < a.nsigs ? a.nsigs - first : 0u) : a.cert_n[c];
     // CS_DOOM: a bad S / undecodable A (the flags say so too) or a vote range overlapping another
     // certificate's (k_expand_count)
-    bool bad = range_bad || (a.cert_state && (a.cert_state[c] & CS_DOOM)), slow = false;
-    uint32_t tsum = 0;
-    uint64_t stake = 0;
-    for (uint32_t v = lane; v < nv; v += 64) {
+    FinalizeAcc r{range_bad || (a.cert_state && (a.cert_state[c] & CS_DOOM)), false, 0u, 0u};
+    for (uint32_t v = t; v < nv; v += stride) {
         const uint32_t f = a.flags[first + v];
         // a vote this certificate does not own (overlapping device ranges, NW_ERR_ARG) was checked
         // against its owner's message: it rejects this certificate and adds none of its stake
         const bool own = a.sig_cert[first + v] == c;
-        bad = bad || !own || ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) || (f & NW_F_R_BAD);
-        slow = slow || (f & NW_F_SLOW);
-        tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
-        if (own && (f & NW_F_STRICT)) stake += a.stake[a.signer[first + v]];
+        r.bad = r.bad || !own || ((f & (NW_F_S_OK | NW_F_A_OK)) != (NW_F_S_OK | NW_F_A_OK)) || (f & NW_F_R_BAD);
+        r.slow = r.slow || (f & NW_F_SLOW);
+        r.tsum += (f >> NW_F_TCOEF_SHIFT) & 7u;
+        if (own && (f & NW_F_STRICT)) r.stake += a.stake[a.signer[first + v]];
     }
-    bad = __any(bad);
-    slow = __any(slow);
+    r.bad = __any(r.bad);
+    r.slow = __any(r.slow);
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
-        tsum += __shfl_xor(tsum, off, 64);
-        stake += __shfl_xor(stake, off, 64);
+        r.tsum += __shfl_xor(r.tsum, off, 64);
+        r.stake += __shfl_xor(r.stake, off, 64);
     }
-    if (lane != 0) return;
-    if (a.accepted_stake) a.accepted_stake[c] = stake;
+    return r;
+}
+
+// Certificate c's verdict from its totals (one thread).
+__device__ __forceinline__ void finalize_decide(const FinalizeParams& a, uint32_t c, const FinalizeAcc& r) {
+    if (a.accepted_stake) a.accepted_stake[c] = r.stake;
     bool ok;
-    if (bad) {
+    if (r.bad) {
         ok = false;
-    } else if (!slow) {
-        ok = (tsum & 7u) == 0;
+    } else if (!r.slow) {
+        ok = (r.tsum & 7u) == 0;
     } else if ((a.cert_state[c] & CS_BIG_MASK) == 1u) {
         ok = false;   // one term with a prime-order component: the sum cannot be the identity (k_slow_prep)
     } else {
@@ -62,6 +71,12 @@ __device__ __forceinline__ void finalize_cert(const FinalizeParams& a, uint32_t 
         return;
     }
     if (a.cert_ok) a.cert_ok[c] = ok ? 1 : 0;
+}
+
+// Certificate c's finalize, by one wave (lane = 0..63).
+__device__ __forceinline__ void finalize_cert(const FinalizeParams& a, uint32_t c, uint32_t lane) {
+    const FinalizeAcc r = finalize_scan(a, c, lane, 64);
+    if (lane == 0) finalize_decide(a, c, r);
 }
 
 // Exact sum of listed certificate c, by one wave (lane = 0..63; part: the wave's LDS rows): every

@@ -53,7 +53,10 @@ extern template hipError_t launch_slow_tail_wa<20>(const VerifyParams&, const Fi
 // serialize: each workgroup histograms a GROUP_TILE-signature tile in LDS and touches global
 // memory once per (tile, slot).  Above GROUP_LDS_KEYS slots the plain global-atomic form is used
 // (contention is then spread over many addresses anyway).
-static constexpr uint32_t GROUP_TILE = 4096;
+#ifndef NW_GROUP_TILE
+#define NW_GROUP_TILE 4096
+#endif
+static constexpr uint32_t GROUP_TILE = NW_GROUP_TILE;
 static constexpr uint32_t GROUP_LDS_KEYS = 8192;
 
 // Out-of-range slots (rejected by k_verify) are grouped with slot 0 so no access leaves the arrays.
@@ -209,6 +212,34 @@ __global__ void __launch_bounds__(256) k_cert_finalize(FinalizeParams a) {
     finalize_cert(a, c, lane);
 }
 
+// One workgroup of NT threads per certificate (launch_finalize: certificates averaging more than
+// 256 votes): the waves' totals meet in LDS.  Same verdicts as k_cert_finalize.
+template <int NT>
+__global__ void __launch_bounds__(NT) k_cert_finalize_wg(FinalizeParams a) {
+    __shared__ uint32_t s_bad, s_slow, s_tsum;
+    __shared__ unsigned long long s_stake;
+    if (a.sig_ok) {
+        const uint32_t nthr = gridDim.x * blockDim.x;
+        for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < a.nsigs; v += nthr)
+            a.sig_ok[v] = (a.flags[v] & NW_F_STRICT) ? 1 : 0;
+    }
+    const uint32_t c = blockIdx.x;   // grid = ncerts
+    if (threadIdx.x == 0) {
+        s_bad = s_slow = s_tsum = 0u;
+        s_stake = 0ull;
+    }
+    __syncthreads();
+    const FinalizeAcc r = finalize_scan(a, c, threadIdx.x, NT);
+    if ((threadIdx.x & 63u) == 0) {
+        if (r.bad) atomicOr(&s_bad, 1u);
+        if (r.slow) atomicOr(&s_slow, 1u);
+        atomicAdd(&s_tsum, r.tsum);
+        atomicAdd(&s_stake, (unsigned long long)r.stake);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) finalize_decide(a, c, FinalizeAcc{s_bad != 0u, s_slow != 0u, s_tsum, (uint64_t)s_stake});
+}
+
 static constexpr uint32_t EXACT_MAX_BLOCKS = 1024;
 __global__ void __launch_bounds__(64) k_cert_exact(FinalizeParams a) {
     __shared__ uint32_t part[64][40];
@@ -230,7 +261,8 @@ __global__ void __launch_bounds__(64) k_cert_tail(FinalizeParams a) {
 // MI355X, dominated by dispatch, not work.
 //   k_prep_certs:   sig_cert = NO_CERT (a vote outside every certificate gets no verdict and no
 //                   exact-path entry), the slot counts, the slow-path counter and the status word = 0.
-//   k_expand_count: block b expands certificates [4 b, 4 b + 4) into sig_cert (a vote already
+//   k_expand_count: block b expands certificates [4 b, 4 b + 4) (fewer, by 2 or 4 waves each, when
+//                   certificates are large) into sig_cert (a vote already
 //                   claimed by another certificate is NW_ERR_ARG: ranges must be disjoint) and, for
 //                   signature tile b (GROUP_TILE signatures), histograms the signer slots (LDS, one
 //                   global add per slot) and/or checks them; every check ORs NW_ERR_ARG into status.
@@ -250,21 +282,24 @@ __global__ void __launch_bounds__(256) k_prep_certs(uint32_t nsigs, uint32_t nke
     if (status && t == 0) *status = 0u;
 }
 
-static constexpr uint32_t EXPAND_CERTS_PER_BLOCK = 4;   // one wave each
+static constexpr uint32_t EXPAND_WAVES_PER_BLOCK = 4;
 __global__ void __launch_bounds__(256) k_expand_count(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys,
                                                       const uint32_t* cert_first, const uint32_t* cert_n,
                                                       const uint32_t* signer, uint32_t* sig_cert, uint32_t* counts,
-                                                      uint32_t* status, uint32_t* cert_state) {
+                                                      uint32_t* status, uint32_t* cert_state, uint32_t wlog) {
     extern __shared__ uint32_t hist[];
-    // one wave per certificate: its lanes write the vote -> certificate entries side by side (a
-    // thread per certificate would store 667 / 6,667 entries serially at C3 / C4)
-    const uint32_t c = blockIdx.x * EXPAND_CERTS_PER_BLOCK + (threadIdx.x >> 6), lane = threadIdx.x & 63u;
+    // 2^wlog waves per certificate: their lanes write the vote -> certificate entries side by side (a
+    // thread per certificate would store 667 / 6,667 entries serially at C3 / C4; one wave, 105
+    // dependent atomic rounds at C4)
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    const uint32_t c = blockIdx.x * (EXPAND_WAVES_PER_BLOCK >> wlog) + (w >> wlog);
+    const uint32_t sub = ((w & ((1u << wlog) - 1u)) << 6) | lane, step = 64u << wlog;
     bool bad = false;
     if (c < ncerts) {
         const uint32_t f = cert_first[c], n = cert_n[c];
-        bad = lane == 0 && (uint64_t)f + n > nsigs;
+        bad = sub == 0 && (uint64_t)f + n > nsigs;
         const uint32_t end = (uint64_t)f + n > nsigs ? nsigs : f + n;   // clamped: k_cert_finalize rejects it
-        for (uint32_t v = f + lane; v < end; v += 64) {
+        for (uint32_t v = f + sub; v < end; v += step) {
             const uint32_t prev = atomicExch(&sig_cert[v], c);
             if (prev != NO_CERT) {
                 // a vote claimed twice: whichever certificate the map ends with checks it against its
@@ -369,7 +404,13 @@ hipError_t launch_finalize(const FinalizeParams& p, hipStream_t st) {
         hipLaunchKernelGGL(k_cert_tail, dim3(1), dim3(64), 0, st, p);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(k_cert_finalize, dim3(blocks_for((uint64_t)p.ncerts * 64, 256)), dim3(256), 0, st, p);
+    const uint64_t avg_votes = p.nsigs / p.ncerts;
+    if (avg_votes > 1024)
+        hipLaunchKernelGGL(k_cert_finalize_wg<1024>, dim3(p.ncerts), dim3(1024), 0, st, p);
+    else if (avg_votes > 256)
+        hipLaunchKernelGGL(k_cert_finalize_wg<256>, dim3(p.ncerts), dim3(256), 0, st, p);
+    else
+        hipLaunchKernelGGL(k_cert_finalize, dim3(blocks_for((uint64_t)p.ncerts * 64, 256)), dim3(256), 0, st, p);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // the exact list's length is on the device: a capped grid that exits at once when it is empty
@@ -384,11 +425,15 @@ hipError_t launch_prep_expand(uint32_t ncerts, uint32_t nsigs, uint32_t nkeys, c
     hipLaunchKernelGGL(k_prep_certs, dim3(prep_blocks), dim3(256), 0, st, nsigs, nkeys, sig_cert, counts, zero4, status,
                        ncerts, cert_state);
     const bool tiles = (counts || status) && nsigs > 0;
-    const uint32_t nb = std::max<uint32_t>(blocks_for(ncerts, EXPAND_CERTS_PER_BLOCK), tiles ? blocks_for(nsigs, GROUP_TILE) : 0u);
+    // waves per certificate from the average vote count (a performance choice only)
+    const uint64_t avg_votes = ncerts ? nsigs / ncerts : 0;
+    const uint32_t wlog = avg_votes > 512 ? 2u : (avg_votes > 128 ? 1u : 0u);
+    const uint32_t nb = std::max<uint32_t>(blocks_for(ncerts, EXPAND_WAVES_PER_BLOCK >> wlog),
+                                           tiles ? blocks_for(nsigs, GROUP_TILE) : 0u);
     if (nb == 0) return hipGetLastError();
     const size_t lds = counts && nkeys <= GROUP_LDS_KEYS ? (size_t)nkeys * 4 : 0;
     hipLaunchKernelGGL(k_expand_count, dim3(nb), dim3(256), lds, st, ncerts, nsigs, nkeys, first, nv, signer, sig_cert,
-                       counts, status, cert_state);
+                       counts, status, cert_state, wlog);
     return hipGetLastError();
 }
 

@@ -2,6 +2,7 @@
 # Per-kernel rocprofv3 averages of the default build vs every build_exp/*.so variant on one bench
 # config.  Usage: KRE='k_finish|k_verify' BENCH_ARGS='--config C4 --steps 6' bash tools/ab_kernel_stats.sh TAG
 set -o pipefail
+shopt -s nullglob
 OUT=gpurun_out/${1:-abk}
 mkdir -p $OUT
 export TMPDIR=/tmp

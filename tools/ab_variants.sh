@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B the libnwcrypto variants in build_exp/ against the default build on the C2 bench (GPU box).
 set -o pipefail
+shopt -s nullglob
 OUT=gpurun_out/${1:-ab}
 mkdir -p $OUT
 ARGS="--steps 20 --warmup 3 --c4-steps 0 --no-cpu-baseline --digest-batches 0 --latency-samples 0 --no-extras ${BENCH_ARGS:-}"
