@@ -560,3 +560,68 @@ def test_sha512_throughput_kernel_many_messages(engine):
     bad = [i for i in range(n)
            if bytes(got[i]) != hashlib.sha512(blob[offs[i]:offs[i] + lens[i]].tobytes()).digest()]
     assert not bad, [(i, int(lens[i]), int(offs[i])) for i in bad[:10]]
+
+
+# ----------------------------------------------------------------------------- large certificates, device ranges
+@pytest.mark.parametrize("votes", [300, 1100])
+def test_large_certificate_device_ranges(votes):
+    """Device-path input checks on certificates large enough for the multi-wave expansion and the
+    workgroup finalize (k_expand_count with 2 / 4 waves per certificate, k_cert_finalize_wg<256> /
+    <1024>; 20 certificates, above the one-wave tail's 16): two overlapping vote ranges (NW_ERR_ARG
+    in the status word, both certificates rejected, neither credited stake it does not own), the
+    votes the shifted range left behind (in no certificate: no verdict), a range running past the
+    signature array (rejected), a forged vote (rejected, as the oracle says; stake one vote short)
+    and honest certificates (accepted with their full stake)."""
+    import torch
+    eng = _engine()
+    try:
+        ncerts, last = 20, 19
+        com, slots, cs = _setup(eng, votes, ncerts, votes)
+        sigs = cs.sigs.copy()
+        forged_cert, forged_vote = 1, 7
+        i = forged_cert * votes + forged_vote
+        sigs[i] = np.frombuffer(nw_ref_sign_other(com, cs, i), np.uint8)
+        first = cs.cert_first.astype(np.int64).copy()
+        n = cs.cert_n.astype(np.int64).copy()
+        first[3] -= 10                      # certificate 3 claims the last 10 votes of certificate 2
+        n[last] += 5                        # the last certificate runs past the signature array
+        gap = np.arange(4 * votes - 10, 4 * votes)   # certificate 3's own last 10 votes: in no range now
+        dev = torch.device("cuda", 0)
+        t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in (
+            ("first", first.astype(np.int32)), ("n", n.astype(np.int32)), ("sigs", sigs),
+            ("signer", slots[cs.signer].astype(np.int32)), ("msgs", cs.msgs))}
+        stake_of = np.asarray(com.stake, np.int64)[cs.signer]
+
+        def span(a, b):
+            return int(stake_of[a:b].sum())
+
+        want = [c not in (1, 2, 3, last) for c in range(ncerts)]
+        for rep in range(3):   # the vote map's atomic order may differ between launches
+            ok = torch.full((ncerts,), 7, dtype=torch.uint8, device=dev)
+            st = torch.full((ncerts,), -1, dtype=torch.int64, device=dev)
+            fl = torch.full((cs.nsigs,), -1, dtype=torch.int32, device=dev)
+            status = torch.full((1,), 99, dtype=torch.int32, device=dev)
+            eng.verify_certs_dev(ncerts, t["first"].data_ptr(), t["n"].data_ptr(), cs.nsigs, t["sigs"].data_ptr(),
+                                 t["signer"].data_ptr(), t["msgs"].data_ptr(), ZSEED, 0, ok.data_ptr(),
+                                 fl.data_ptr(), st.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                                 d_status=status.data_ptr())
+            torch.cuda.synchronize()
+            assert int(status.item()) == 2, rep
+            assert ok.cpu().numpy().astype(bool).tolist() == want, rep
+            stk = st.cpu().numpy()
+            for c in range(ncerts):
+                if want[c]:
+                    assert stk[c] == span(c * votes, (c + 1) * votes), (rep, c)
+            assert stk[forged_cert] == span(votes, 2 * votes) - int(stake_of[i]), rep
+            # certificate 2 owns its first votes - 10 for sure and the shared 10 if it won them (they
+            # verify under its message); certificate 3's shared votes never verify under its message
+            assert span(2 * votes, 3 * votes - 10) <= stk[2] <= span(2 * votes, 3 * votes), (rep, stk[2])
+            assert stk[3] == span(3 * votes, 4 * votes - 10), (rep, stk[3])
+            assert (fl.cpu().numpy()[gap] == 0).all(), rep
+        # the forged certificate's verdict from the oracle (its own votes, batch index = its index)
+        f0, nv = int(cs.cert_first[forged_cert]), int(cs.cert_n[forged_cert])
+        pks = [bytes(com.pks[k]) for k in cs.signer[f0:f0 + nv]]
+        assert not nw_ref.verify_batch_msgs([bytes(cs.msgs[forged_cert])] * nv, pks,
+                                            [bytes(x) for x in sigs[f0:f0 + nv]], ZSEED, forged_cert)
+    finally:
+        eng.close()
