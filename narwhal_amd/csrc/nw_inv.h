@@ -292,11 +292,14 @@ __device__ __forceinline__ fe fe_invert_batched(const fe& z) {
 }
 
 // z^-1 for every lane of a workgroup of NWAVES full waves (every thread of the block calls it, one
-// value per lane): the wave butterfly as above, then the NWAVES wave products meet in LDS and wave 0
-// runs the block's ONE scalar-unit inversion; slot is __shared__ scratch of (NWAVES + 1) x 10 words.
-// A CU's waves share one scalar unit, so with several waves per SIMD this cuts its work NWAVES-fold.
+// value per lane; 2 <= NWAVES <= 64, a power of two): the wave butterfly as above, then the NWAVES
+// wave products meet in LDS, where wave 0 runs the same butterfly over them (lane w holds wave w's
+// product), the block's ONE scalar-unit inversion, and hands every wave the inverse of its own
+// product.  slot: __shared__ scratch of NWAVES x 10 words.  A CU's waves share one scalar unit, so
+// with several waves per SIMD this cuts its work NWAVES-fold.
 template <int NWAVES>
 __device__ __forceinline__ fe fe_invert_block(const fe& z, uint32_t (*slot)[10]) {
+    static_assert(NWAVES >= 2 && NWAVES <= 64 && (NWAVES & (NWAVES - 1)) == 0, "NWAVES: a power of two");
     const bool zz = fe_iszero(z);
     fe t = fe_select(z, fe_one(), zz);
     fe others = fe_one();
@@ -306,33 +309,38 @@ __device__ __forceinline__ fe fe_invert_block(const fe& z, uint32_t (*slot)[10])
         others = fe_mul(others, p);
         t = fe_mul(t, p);
     }
-    const uint32_t w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63u) == 0) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+    if (lane == 0) {
 #pragma unroll
         for (int k = 0; k < 10; ++k) slot[w][k] = t.v[k];
     }
     __syncthreads();
-    fe ow = fe_one();   // product of the other waves' products
-#pragma unroll
-    for (int v = 0; v < NWAVES; ++v) {
-        if ((uint32_t)v == w) continue;
-        fe tv;
-#pragma unroll
-        for (int k = 0; k < 10; ++k) tv.v[k] = slot[v][k];
-        ow = fe_mul(ow, tv);
-    }
     if (w == 0) {
-        const fe inv = fe_invert_wave(fe_mul(ow, t));
-        if (threadIdx.x == 0) {
+        // lanes [0, NWAVES) hold the wave products; the xor levels below NWAVES keep every group of
+        // NWAVES lanes to itself, so lanes past NWAVES (ones) never reach group 0
+        fe v = fe_one();
+        if (lane < (uint32_t)NWAVES) {
 #pragma unroll
-            for (int k = 0; k < 10; ++k) slot[NWAVES][k] = inv.v[k];
+            for (int k = 0; k < 10; ++k) v.v[k] = slot[lane][k];
+        }
+        fe vo = fe_one();
+#pragma unroll
+        for (int off = 1; off < NWAVES; off <<= 1) {
+            const fe p = fe_shfl_xor(v, off);
+            vo = fe_mul(vo, p);
+            v = fe_mul(v, p);
+        }
+        const fe r = fe_mul(fe_invert_wave(v), vo);   // lane w < NWAVES: (wave w's product)^-1
+        if (lane < (uint32_t)NWAVES) {
+#pragma unroll
+            for (int k = 0; k < 10; ++k) slot[lane][k] = r.v[k];
         }
     }
     __syncthreads();
-    fe inv;
+    fe tw;
 #pragma unroll
-    for (int k = 0; k < 10; ++k) inv.v[k] = slot[NWAVES][k];
-    const fe r = fe_mul(fe_mul(inv, ow), others);
+    for (int k = 0; k < 10; ++k) tw.v[k] = slot[w][k];
+    const fe r = fe_mul(tw, others);
     return fe_select(r, fe_zero(), zz);
 }
 #endif

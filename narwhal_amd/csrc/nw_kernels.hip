@@ -138,8 +138,12 @@ __global__ void __launch_bounds__(256) k_scatter_slots_lds(uint32_t n, uint32_t 
 // inversion (fe_invert_block).  Round 6 first ran the chains fully unrolled with every load hoisted
 // (256 VGPRs, one wave per SIMD, a wave-batched inversion each): latency-bound, 1.17 ms per 8.3 M
 // signatures at C4 against 0.56 ms now, 126 against 104 us at C2 (profiles/r06/finish_ab_r06.txt).
+// chunked k_finish workgroup: one inversion each.  512 / 1,024 threads (fewer inversions sharing a
+// CU's scalar unit) measured slower at C2 and C4: 155 / 111 us against 104 us per C2 step
+// (profiles/r06/finish_ab_r06.txt)
+static constexpr uint32_t FINISH_WG = 256;
 template <bool ONE>
-__global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
+__global__ void __launch_bounds__(ONE ? 256 : FINISH_WG) k_finish(VerifyParams a) {
     const uint32_t NL = (a.gn + a.fk - 1) / a.fk;
     const uint32_t Lr = blockIdx.x * blockDim.x + threadIdx.x;
     // A wave (ONE) or a workgroup (chunked: fe_invert_block synchronizes it) with any owned lane
@@ -164,7 +168,7 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
         const uint32_t f = finish_x_flags(X, zi, pf);
         if (owner) emit(i, pf, f);
     } else {
-        __shared__ uint32_t inv_slot[5][10];
+        __shared__ uint32_t inv_slot[FINISH_WG / 64][10];
         const uint32_t* zrow = a.pbuf + 10 * n;
         fe acc = fe_one();
         fe znext = load_fe_soa(zrow, n, gbase);
@@ -177,7 +181,7 @@ __global__ void __launch_bounds__(256) k_finish(VerifyParams a) {
             // the last prefix is never read back; duplicates store the owner's own values (scratch)
             if (k + 1 < cnt) store_fe_soa(a.pre, n, g, acc);
         }
-        fe inv = fe_invert_block<4>(acc, inv_slot);
+        fe inv = fe_invert_block<FINISH_WG / 64>(acc, inv_slot);
 #pragma unroll 1
         for (int k = (int)cnt - 1; k >= 0; --k) {
             const size_t g = gbase + (size_t)k * NL;
@@ -394,7 +398,7 @@ hipError_t launch_finish(const VerifyParams& p, hipStream_t st) {
     if (p.fk < 1 || p.fk > (uint32_t)FINISH_K || (uint64_t)p.g0 + p.gn > p.n) return hipErrorInvalidValue;
     const uint64_t lanes = (p.gn + p.fk - 1) / p.fk;
     if (p.fk == 1) hipLaunchKernelGGL(k_finish<true>, dim3(blocks_for(lanes, 256)), dim3(256), 0, st, p);
-    else hipLaunchKernelGGL(k_finish<false>, dim3(blocks_for(lanes, 256)), dim3(256), 0, st, p);
+    else hipLaunchKernelGGL(k_finish<false>, dim3(blocks_for(lanes, FINISH_WG)), dim3(FINISH_WG), 0, st, p);
     return hipGetLastError();
 }
 
