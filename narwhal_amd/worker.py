@@ -176,7 +176,12 @@ def serialize_worker_primary_message(digest32: bytes, worker_id: int, own_digest
 class DigestBatcher:
     """Windows of batches -> one asynchronous GPU submission each; results in arrival order."""
 
-    def __init__(self, engine=None, window: int = 64, depth: int = 2, max_bytes: int = 256 << 20):
+    # max_bytes: a window is cut into several submissions only above 1 GiB of batches.  C4's
+    # per-GPU window (1,250 x 508,052 B = 635 MB) as ONE submission: 41.2-41.7 k batches/s against
+    # 21.0-22.0 k when a 256 MiB cap cut it into three jobs (depth 2 or 4: concurrent jobs of one
+    # context do not overlap their digests, profiles/r06/worker_window_r06.txt).  The price is one
+    # pinned staging buffer of the window's size per workspace in flight.
+    def __init__(self, engine=None, window: int = 64, depth: int = 2, max_bytes: int = 1 << 30):
         if window < 1 or depth < 1:
             raise ValueError("window and depth must be >= 1")
         self.engine = engine or _lib.default_engine()
