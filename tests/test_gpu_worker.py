@@ -6,6 +6,7 @@ narwhal_amd.worker) against hashlib and the reference's own Processor test.
 * 150 batches in arrival order through windows of 16 with 3 in flight: C4-shape bincode batches
   (508,052 B, node/src/benchmark_client.rs tx layout), small and empty batches, unaligned host
   buffers, partial windows flushed mid-stream;
+* C4's 635 MB window as one submission (default byte cap), then a second window;
 * the raw ABI: a job polls not-done/done, an empty job, jobs waited out of submission order.
 """
 import hashlib
@@ -65,6 +66,32 @@ def test_batched_digests_in_arrival_order(engine):
         assert x is want
         assert d == hashlib.sha512(bytes(want)).digest()
     assert b.submissions >= len(batches) // 16
+
+
+def test_c4_window_is_one_submission(engine):
+    """C4's per-GPU window (1,250 x 508,052 B = 635 MB, worker/src/processor.rs:63-65 for each
+    batch) goes out as ONE nw_sha512_many_async job under the default byte cap, every digest equal
+    to hashlib's; a second window follows through the same batcher (pinned buffer reuse)."""
+    from narwhal_amd import worker, workload
+    host = workload.worker_batches_np(1250)
+    rows = [host[i].copy() for i in range(1250)]
+    for k in range(0, 1250, 97):                    # distinct contents along the window
+        rows[k][100:108] = np.frombuffer(struct.pack("<Q", k + 1), np.uint8)
+    b = worker.DigestBatcher(engine, window=1250, depth=2)
+    got = []
+    for x in rows:
+        b.push(x)
+        got += b.ready()
+    assert b.submissions == 1
+    tail = [r.copy() for r in rows[:300]]
+    for x in tail:
+        b.push(x)
+    got += b.drain()
+    assert b.submissions == 2
+    assert len(got) == 1550
+    for (d, x), want in zip(got, rows + tail):
+        assert x is want
+        assert d == hashlib.sha512(want.tobytes()).digest()
 
 
 def test_async_abi_poll_and_out_of_order_wait(engine):
